@@ -1,0 +1,193 @@
+/*
+ * rl_abi.h — C-ABI of the MI355X batched raceline optimizer (steps 7–8 of the
+ * reference pipeline).
+ *
+ * This is the drop-in boundary.  Each entry point replaces one reference
+ * function.  "ref" means /root/reference/src/main.cpp (snapshot 2025-10-17).
+ *
+ *   rl_optimize / rl_plan_*   replace
+ *       raceline_min_curv::compute_min_curvature_raceline   (ref:683-764)
+ *       raceline_min_time::compute_min_time_raceline         (ref:905-1052)
+ *     as called from pipeline::compute_raceline_and_save     (ref:1347-1348)
+ *     and pipeline::compute_mintime_and_save                  (ref:1397-1398).
+ *   rl_cfg                    mirrors the hot-path subset of cfg::Config (ref:47-119).
+ *   rl_cfg_default            mirrors the cfg::Config default initialisers (ref:77-113).
+ *   rl_ring_segments          mirrors edges::ringEdges / edges::polylineEdges (ref:251-260).
+ *
+ * Conventions:
+ *   - Plain C types only; the caller owns every buffer; no exception crosses the ABI.
+ *   - Return value 0 on success, a negative RL_E* code on failure; rl_last_error()
+ *     returns a human-readable message for the calling thread.
+ *   - All arithmetic is IEEE fp64.  Points are interleaved [N][2] (x,y), like the
+ *     reference's vector<Vec2>.  Segments are [E][4] (x0,y0,x1,y1), like the
+ *     reference's vector<pair<Vec2,Vec2>>.
+ *   - Results are structure-of-arrays [B][N] (instance-major).
+ *   - The compute path is the HIP/gfx950 kernel.  There is no CPU fallback:
+ *     with no usable GPU every compute entry point returns RL_ENODEV.
+ */
+#ifndef RL_ABI_H
+#define RL_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RL_ABI_VERSION 1
+
+/* error codes */
+#define RL_OK          0
+#define RL_EINVAL     -1   /* bad argument (NULL pointer, N<0, B<1, n_cfg not 1 or B, ...) */
+#define RL_ENODEV     -2   /* no HIP device / device not usable                           */
+#define RL_EHIP       -3   /* a HIP runtime call failed                                   */
+#define RL_ENOMEM     -4   /* device or host allocation failed                            */
+#define RL_ETOOBIG    -5   /* N exceeds what the selected kernel supports                 */
+
+/* optimisation modes (bitmask for rl_plan_create) */
+#define RL_MODE_MINCURV 1  /* compute_min_curvature_raceline (ref:683) */
+#define RL_MODE_MINTIME 2  /* compute_min_time_raceline      (ref:905) */
+
+/*
+ * Hot-path knobs of cfg::Config (ref:47-119).  Field names and meanings are the
+ * reference's.  Note the static-initialisation quirk (ref:102): a_total_max is
+ * NOT derived from mu at run time; rl_cfg_set_mu() recomputes it the way a
+ * recompiled reference would (mu*9.81).
+ */
+typedef struct rl_cfg {
+    double  veh_width_m;         /* ref:77  corridor updates use this (ref:753, 1037)   */
+    double  safety_margin_m;     /* ref:78                                               */
+    double  lambda_smooth;       /* ref:81                                               */
+    int32_t max_outer_iters;     /* ref:82                                               */
+    int32_t max_inner_iters;     /* ref:83                                               */
+    double  step_init;           /* ref:84                                               */
+    double  step_min;            /* ref:85                                               */
+    double  armijo_c;            /* ref:86                                               */
+    double  kappa_eps;           /* ref:89                                               */
+    double  v_cap_mps;           /* ref:90                                               */
+    double  mass_kg;             /* ref:93                                               */
+    double  Cd;                  /* ref:94                                               */
+    double  A_front_m2;          /* ref:95                                               */
+    double  rho_air;             /* ref:96                                               */
+    double  c_rr;                /* ref:97                                               */
+    double  P_max_W;             /* ref:98                                               */
+    double  mu;                  /* ref:101 (informational: the hot path reads a_total_max) */
+    double  a_total_max;         /* ref:102                                              */
+    double  a_lat_max;           /* ref:103                                              */
+    double  a_long_acc_cap;      /* ref:104                                              */
+    double  a_long_brake_cap;    /* ref:105                                              */
+    double  w_time_gain;         /* ref:108                                              */
+    double  time_gamma_power;    /* ref:109                                              */
+    int32_t time_weight_use_inv_v; /* ref:110 (bool)                                     */
+    int32_t max_vpass_iters;     /* ref:112                                              */
+    double  inv_v_gain;          /* ref:111                                              */
+    int32_t use_total_ge_lat;    /* ref:113 (bool)                                       */
+    int32_t _pad0;
+} rl_cfg;
+
+/*
+ * One track problem: the inputs of compute_*_raceline (ref:683-686, 905-909).
+ *   center_xy  [N][2]   centerline samples (closing duplicate already popped, ref:1681-1683)
+ *   L                   spline arc length (ref:464); h = L/N (ref:690, 913)
+ *   inner_seg  [Ei][4]  inner ring segments (ringEdges / polylineEdges of inner_from_mids)
+ *   outer_seg  [Eo][4]  outer ring segments
+ *   veh_width           the function argument used for the INITIAL corridor only (ref:706, 930)
+ *   closed              closed-loop (periodic) operators when nonzero
+ */
+typedef struct rl_problem {
+    const double* center_xy;
+    int32_t       N;
+    int32_t       closed;
+    double        L;
+    const double* inner_seg;
+    int32_t       Ei;
+    int32_t       Eo;
+    const double* outer_seg;
+    double        veh_width;
+} rl_problem;
+
+/*
+ * Caller-allocated results, structure-of-arrays, instance-major [B][N].
+ * Any pointer may be NULL to skip that output.  v / ax / lap / vpass_sweeps are
+ * written for RL_MODE_MINTIME only.
+ *   evals        [B][max_outer_iters]   cost/grad evaluations per outer iteration
+ *                                       (the E_k of SURVEY.md §3; 0 for skipped outers)
+ *   accepts      [B][max_outer_iters]   accepted PGD steps per outer iteration
+ *   vpass_sweeps [B][max_outer_iters+1] v-pass sweeps actually executed per call
+ *                                       (early exit once a sweep changes nothing is exact)
+ */
+typedef struct rl_out {
+    double*  x;
+    double*  y;
+    double*  heading;
+    double*  kappa;
+    double*  alpha_total;
+    double*  alpha_last;
+    double*  v;
+    double*  ax;
+    double*  lap;
+    int32_t* evals;
+    int32_t* accepts;
+    int32_t* vpass_sweeps;
+} rl_out;
+
+/* ---------------------------------------------------------------- config */
+void rl_cfg_default(rl_cfg* cfg);
+/* mu sweep helper: sets mu and a_total_max = mu*9.81 (ref:101-102) */
+void rl_cfg_set_mu(rl_cfg* cfg, double mu);
+
+/* ------------------------------------------------------------- geometry
+ * Ring → segments, like edges::ringEdges (closed, ref:251-255: n segments with wrap)
+ * or edges::polylineEdges (open, ref:256-260: n-1 segments).  seg_out must hold
+ * [n][4] doubles.  Returns the number of segments written (>=0) or RL_EINVAL.     */
+int rl_ring_segments(const double* ring_xy, int32_t n, int32_t closed, double* seg_out);
+
+/* α-seed of instance b at sample i (build-defined):
+ *   seed 0            -> 0.0 (the reference starts from α≡0, ref:720)
+ *   otherwise         -> sigma * xi, xi ~ U(-1,1) from splitmix64(seed, i),
+ * clamped to the initial corridor [lo_i, hi_i] by the optimizer itself.          */
+double rl_seed_value(uint64_t seed, int32_t i, double sigma);
+#define RL_SEED_SIGMA 0.25
+
+/* ------------------------------------------------------------ one-shot
+ * Optimise B instances of one problem.  cfg has n_cfg entries (1 = broadcast,
+ * or B = one per instance).  seeds has B entries or is NULL (all zero = exactly
+ * the reference).  out_mincurv / out_mintime may be NULL to skip that mode.
+ * Synchronous: host buffers in, host buffers out (PCIe included).               */
+int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
+                const uint64_t* seeds, int32_t B,
+                rl_out* out_mincurv, rl_out* out_mintime);
+
+/* ---------------------------------------------------- device-resident plan
+ * For repeated runs with inputs already resident in HBM (bench, services).
+ * create: allocates device buffers on `device` and uploads the inputs.
+ * run:    enqueues the optimisation on `hip_stream` (a hipStream_t; NULL = the
+ *         plan's own stream) and returns immediately.
+ * fetch:  copies results to host (synchronises the stream used by run).
+ * device_outputs: device pointers of the result arrays (for collectives).       */
+typedef struct rl_plan rl_plan;
+
+int rl_plan_create(rl_plan** plan, int32_t device, const rl_problem* prob,
+                   const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds,
+                   int32_t B, int32_t modes);
+int rl_plan_run(rl_plan* plan, void* hip_stream);
+int rl_plan_fetch(rl_plan* plan, rl_out* out_mincurv, rl_out* out_mintime);
+/* which: RL_MODE_MINCURV or RL_MODE_MINTIME; fills device pointers (same layout as
+ * rl_out, NULL where the mode does not produce the field). */
+int rl_plan_device_outputs(rl_plan* plan, int32_t which, rl_out* dev_out);
+/* per-kernel device time of the last run, in ms, measured with HIP events on the
+ * run stream (index 0 = main optimisation kernel, 1 = prepare, 2 = finalize).  */
+int rl_plan_kernel_ms(rl_plan* plan, int32_t idx, float* ms);
+int rl_plan_destroy(rl_plan* plan);
+
+/* ------------------------------------------------------------- runtime */
+int         rl_device_count(void);
+const char* rl_last_error(void);
+int         rl_abi_version(void);
+/* kernel variant the library would pick for N (samples per lane), or RL_ETOOBIG */
+int         rl_kernel_variant(int32_t N);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RL_ABI_H */

@@ -1,0 +1,112 @@
+"""ctypes access to the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The oracle is the checker, never the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from practice_path_planning_for_formula_student_driverless_amd import abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref_harness.so")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+_ORACLE = None
+
+
+def build_oracle() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so"], check=True)
+
+
+def oracle() -> C.CDLL:
+    global _ORACLE
+    if _ORACLE is None:
+        if not os.path.exists(ORACLE_SO):
+            build_oracle()
+        lib = C.CDLL(ORACLE_SO)
+        abi.declare_optimize(lib.oracle_optimize)
+        lib.oracle_optimize_range.restype = C.c_int
+        lib.oracle_optimize_range.argtypes = [C.POINTER(abi.RlProblem), C.POINTER(abi.RlCfg), C.c_int32,
+                                              C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_int32,
+                                              C.POINTER(abi.RlOut), C.POINTER(abi.RlOut)]
+        lib.oracle_cfg_default.argtypes = [C.POINTER(abi.RlCfg)]
+        lib.oracle_seed_value.argtypes = [C.c_uint64, C.c_int32, C.c_double]
+        lib.oracle_seed_value.restype = C.c_double
+        lib.oracle_vpass.argtypes = [C.POINTER(abi.RlCfg), C.POINTER(C.c_double), C.c_int, C.c_double, C.c_int,
+                                     C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32)]
+        lib.oracle_vpass.restype = C.c_double
+        lib.oracle_ring_segments.argtypes = [C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_double)]
+        lib.oracle_ring_segments.restype = C.c_int
+        _ORACLE = lib
+    return _ORACLE
+
+
+def oracle_cfg_default() -> abi.RlCfg:
+    c = abi.RlCfg()
+    oracle().oracle_cfg_default(C.byref(c))
+    return c
+
+
+def ring_segments(ring: np.ndarray, closed: bool) -> np.ndarray:
+    ring = np.ascontiguousarray(ring, dtype=np.float64).reshape(-1, 2)
+    seg = np.zeros((max(len(ring), 1), 4))
+    n = oracle().oracle_ring_segments(abi.dptr(ring), len(ring), 1 if closed else 0, abi.dptr(seg))
+    return seg[:n].copy()
+
+
+def run_oracle(prob: abi.Problem, cfgs, seeds=None, B: int = 1, modes=(True, True), b_range=None):
+    """Run the C oracle.  Returns (Outputs|None for min-curv, Outputs|None for min-time)."""
+    cfg_arr, ncfg = abi.cfg_array(cfgs)
+    mo = int(cfg_arr[0].max_outer_iters)
+    seeds_a = abi.seed_array(seeds)
+    out_mc = abi.Outputs.alloc(B, prob.N, mo, False) if modes[0] else None
+    out_mt = abi.Outputs.alloc(B, prob.N, mo, True) if modes[1] else None
+    c_mc = out_mc.as_c() if out_mc else None
+    c_mt = out_mt.as_c() if out_mt else None
+    p = prob.as_c()
+    b0, b1 = b_range if b_range else (0, B)
+    rc = oracle().oracle_optimize_range(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B, b0, b1,
+                                        C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle_optimize failed rc={rc}")
+    return out_mc, out_mt
+
+
+def load_case(name: str) -> dict:
+    """Load a golden fixture (npz, no pickle) + its manifest entry."""
+    import json
+
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        man = json.load(f)
+    entry = man["cases"][name]
+    data = dict(np.load(os.path.join(GOLDEN, entry["file"]), allow_pickle=False))
+    data["_meta"] = entry
+    return data
+
+
+def case_problem(case: dict) -> abi.Problem:
+    meta = case["_meta"]
+    closed = bool(meta["closed"])
+    return abi.Problem(center=case["center"], L=float(case["L"]),
+                       inner_seg=ring_segments(case["inner_ring"], closed),
+                       outer_seg=ring_segments(case["outer_ring"], closed),
+                       veh_width=float(meta["veh_width"]), closed=closed)
+
+
+def case_cfg(case: dict) -> abi.RlCfg:
+    return abi.RlCfg.from_dict(case["_meta"]["cfg"])
+
+
+def manifest() -> dict:
+    import json
+
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
