@@ -1,0 +1,91 @@
+"""Build the native pieces in-tree (they travel to the GPU box with the snapshot).
+
+  _lib/librl.so          HIP kernels for gfx950 + the C-ABI (include/rl_abi.h)
+  _lib/fsd_raceline      single-file C++17 host CLI (host/raceline.cpp) over the C-ABI
+  oracle/liboracle.so    CPU checker (test infrastructure, see oracle/)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+LIB_DIR = os.path.join(PKG, "_lib")
+INCLUDE = os.path.join(REPO, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+KERNEL_SRCS = ["csrc/rl_kernels.hip", "csrc/rl_abi.cpp"]
+KERNEL_DEPS = KERNEL_SRCS + ["csrc/rl_kernels.h", "csrc/rl_device.h", "csrc/rl_math.h"]
+# -ffp-contract=off: HIP defaults to fusing a*b+c into FMA, which would change
+# the reference's roundings.
+HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+             "-I" + INCLUDE, "-Wno-unused-command-line-argument"]
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(os.path.join(PKG, d) if not os.path.isabs(d) else d) > t for d in deps)
+
+
+def _run(cmd, cwd=None):
+    r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}")
+    return r.stdout
+
+
+def build_lib(force: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    out = os.path.join(LIB_DIR, "librl.so")
+    deps = KERNEL_DEPS + [os.path.join(INCLUDE, "rl_abi.h")]
+    if force or _stale(out, deps):
+        tmp = out + ".tmp"
+        _run([HIPCC, *HIP_FLAGS, "-shared", *KERNEL_SRCS, "-o", tmp], cwd=PKG)
+        os.replace(tmp, out)
+    return out
+
+
+def build_host(force: bool = False) -> str:
+    """host/raceline.cpp -> _lib/fsd_raceline, linked against librl.so (rpath $ORIGIN)."""
+    lib = build_lib(force)
+    out = os.path.join(LIB_DIR, "fsd_raceline")
+    src = os.path.join(PKG, "host", "raceline.cpp")
+    if not os.path.exists(src):
+        return ""
+    if force or _stale(out, [src, lib, os.path.join(INCLUDE, "rl_abi.h")]):
+        cxx = shutil.which("g++") or "c++"
+        _run([cxx, "-std=c++17", "-O2", "-ffp-contract=off", "-I" + INCLUDE, src, "-o", out,
+              "-L" + LIB_DIR, "-lrl", "-Wl,-rpath,$ORIGIN"], cwd=PKG)
+    return out
+
+
+def build_oracle() -> str:
+    _run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "liboracle.so"])
+    return os.path.join(REPO, "oracle", "liboracle.so")
+
+
+def build_ref_oracle() -> str:
+    """oracle/_ref: the reference compiled from /root/reference where it lies (build container only)."""
+    if not os.path.exists("/root/reference/src/main.cpp"):
+        return ""
+    _run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
+    return os.path.join(REPO, "oracle", "_ref", "libref_harness.so")
+
+
+def build_all(force: bool = False) -> None:
+    build_lib(force)
+    build_host(force)
+    build_oracle()
+    build_ref_oracle()
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("built:", os.listdir(LIB_DIR))

@@ -1,0 +1,381 @@
+// rl_abi.cpp — C-ABI implementation (include/rl_abi.h): argument checks, device
+// buffers, one HIP stream per plan, HIP-event timing.  The compute path is the
+// gfx950 kernel in rl_kernels.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rl_abi.h"
+#include "rl_device.h"
+#include "rl_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess) return fail(RL_EHIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// std::max (ref:506 uses std::max(1e-30, ...))
+inline double smax_h(double a, double b) { return (a < b) ? b : a; }
+
+// Segment records from [E][4] (x0,y0,x1,y1); vx,vy,denom exactly as the reference
+// computes them (ref:482, 505-506).  mx,my,hr for conservative culling.
+void make_segrecs(const double* s, int E, std::vector<rl::SegRec>& out) {
+    for (int e = 0; e < E; ++e) {
+        rl::SegRec r;
+        r.x0 = s[4 * e];
+        r.y0 = s[4 * e + 1];
+        r.vx = s[4 * e + 2] - s[4 * e];
+        r.vy = s[4 * e + 3] - s[4 * e + 1];
+        r.denom = smax_h(1e-30, r.vx * r.vx + r.vy * r.vy);
+        r.mx = 0.5 * (s[4 * e] + s[4 * e + 2]);
+        r.my = 0.5 * (s[4 * e + 1] + s[4 * e + 3]);
+        r.hr = 0.5 * std::sqrt(r.vx * r.vx + r.vy * r.vy) * (1.0 + 1e-9) + 1e-12;
+        out.push_back(r);
+    }
+}
+
+struct ModeBufs {
+    double *x = nullptr, *y = nullptr, *heading = nullptr, *kappa = nullptr, *alpha_total = nullptr,
+           *alpha_last = nullptr, *v = nullptr, *ax = nullptr, *lap = nullptr, *nx = nullptr, *ny = nullptr;
+    int32_t *evals = nullptr, *accepts = nullptr, *sweeps = nullptr;
+};
+
+}  // namespace
+
+struct rl_plan {
+    int device = 0;
+    int N = 0, B = 0, modes = 0, ncfg = 0, max_outer = 0, closed = 1, Ei = 0, Eo = 0;
+    double L = 0, veh_width = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool ran = false;
+    double* d_center = nullptr;
+    rl::SegRec* d_seg = nullptr;
+    rl_cfg* d_cfg = nullptr;
+    uint64_t* d_seeds = nullptr;
+    ModeBufs mb[2];
+    std::vector<void*> allocs;
+
+    template <class T>
+    int alloc(T** p, size_t n) {
+        if (n == 0) n = 1;
+        hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+        if (e != hipSuccess) return fail(RL_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        allocs.push_back((void*)*p);
+        return RL_OK;
+    }
+};
+
+extern "C" {
+
+const char* rl_last_error(void) { return g_err.c_str(); }
+int rl_abi_version(void) { return RL_ABI_VERSION; }
+
+int rl_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rl_kernel_variant(int32_t N) {
+    int k = rl::pick_k(N);
+    return k < 0 ? RL_ETOOBIG : k;
+}
+
+// cfg::Config defaults, ref:77-113
+void rl_cfg_default(rl_cfg* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->veh_width_m = 1.0;
+    c->safety_margin_m = 0.05;
+    c->lambda_smooth = 1.6e-3;
+    c->max_outer_iters = 14;
+    c->max_inner_iters = 120;
+    c->step_init = 0.65;
+    c->step_min = 1e-6;
+    c->armijo_c = 1e-5;
+    c->kappa_eps = 1e-6;
+    c->v_cap_mps = 27.0;
+    c->mass_kg = 255.0;
+    c->Cd = 0.30;
+    c->A_front_m2 = 1.00;
+    c->rho_air = 1.225;
+    c->c_rr = 0.015;
+    c->P_max_W = 80000.0;
+    c->mu = 1.17;
+    c->a_total_max = c->mu * 9.81;   // ref:102 (evaluated once)
+    c->a_lat_max = 11.0;
+    c->a_long_acc_cap = 8.0;
+    c->a_long_brake_cap = 11.0;
+    c->w_time_gain = 1.0;
+    c->time_gamma_power = 2.0;
+    c->time_weight_use_inv_v = 0;
+    c->inv_v_gain = 0.1;
+    c->max_vpass_iters = 6;
+    c->use_total_ge_lat = 1;
+}
+
+void rl_cfg_set_mu(rl_cfg* c, double mu) {
+    if (!c) return;
+    c->mu = mu;
+    c->a_total_max = mu * 9.81;
+}
+
+// edges::ringEdges ref:251-255 / edges::polylineEdges ref:256-260
+int rl_ring_segments(const double* ring_xy, int32_t n, int32_t closed, double* seg_out) {
+    if (n < 0 || (n > 0 && (!ring_xy || !seg_out))) return fail(RL_EINVAL, "rl_ring_segments: bad argument");
+    if (closed) {
+        for (int i = 0; i < n; ++i) {
+            int j = (i + 1) % n;
+            seg_out[4 * i] = ring_xy[2 * i];
+            seg_out[4 * i + 1] = ring_xy[2 * i + 1];
+            seg_out[4 * i + 2] = ring_xy[2 * j];
+            seg_out[4 * i + 3] = ring_xy[2 * j + 1];
+        }
+        return n;
+    }
+    if (n < 2) return 0;
+    for (int i = 0; i + 1 < n; ++i) {
+        seg_out[4 * i] = ring_xy[2 * i];
+        seg_out[4 * i + 1] = ring_xy[2 * i + 1];
+        seg_out[4 * i + 2] = ring_xy[2 * i + 2];
+        seg_out[4 * i + 3] = ring_xy[2 * i + 3];
+    }
+    return n - 1;
+}
+
+double rl_seed_value(uint64_t seed, int32_t i, double sigma) { return rl::seed_value(seed, i, sigma); }
+
+int rl_plan_destroy(rl_plan* plan) {
+    if (!plan) return RL_OK;
+    hipSetDevice(plan->device);
+    if (plan->last_stream) hipStreamSynchronize(plan->last_stream);
+    for (void* p : plan->allocs) hipFree(p);
+    for (auto& e : plan->ev)
+        if (e) hipEventDestroy(e);
+    if (plan->own_stream) hipStreamDestroy(plan->own_stream);
+    delete plan;
+    return RL_OK;
+}
+
+int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
+                   const uint64_t* seeds, int32_t B, int32_t modes) {
+    if (!out) return fail(RL_EINVAL, "plan out pointer is NULL");
+    *out = nullptr;
+    if (!prob || !cfg) return fail(RL_EINVAL, "problem/cfg is NULL");
+    if (B < 1) return fail(RL_EINVAL, "B must be >= 1");
+    if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
+    if (prob->N < 0) return fail(RL_EINVAL, "N < 0");
+    if ((modes & (RL_MODE_MINCURV | RL_MODE_MINTIME)) == 0 || (modes & ~3)) return fail(RL_EINVAL, "bad modes");
+    if (prob->N > 0 && (!prob->center_xy || !(prob->L > 0) || !std::isfinite(prob->L)))
+        return fail(RL_EINVAL, "center_xy NULL or L not positive/finite");
+    if (prob->Ei < 0 || prob->Eo < 0 || (prob->Ei > 0 && !prob->inner_seg) || (prob->Eo > 0 && !prob->outer_seg))
+        return fail(RL_EINVAL, "bad segments");
+    const int mo = cfg[0].max_outer_iters;
+    for (int c = 0; c < n_cfg; ++c) {
+        if (cfg[c].max_outer_iters != mo) return fail(RL_EINVAL, "max_outer_iters must be equal across cfgs");
+        if (cfg[c].max_outer_iters < 0 || cfg[c].max_inner_iters < 0 || cfg[c].max_vpass_iters < 0)
+            return fail(RL_EINVAL, "negative iteration count");
+    }
+    if (prob->N > 0 && rl::pick_k(prob->N) < 0)
+        return fail(RL_ETOOBIG, "N exceeds the register-resident kernel (N <= 4096)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+
+    rl_plan* p = new rl_plan();
+    p->device = device;
+    p->N = prob->N;
+    p->B = B;
+    p->modes = modes;
+    p->ncfg = n_cfg;
+    p->max_outer = mo;
+    p->closed = prob->closed ? 1 : 0;
+    p->L = prob->L;
+    p->veh_width = prob->veh_width;
+    p->Ei = prob->Ei;
+    p->Eo = prob->Eo;
+    int rc = RL_OK;
+    auto cleanup = [&](int code) {
+        rl_plan_destroy(p);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(RL_EHIP, "hipStreamCreate failed"));
+    for (auto& e : p->ev)
+        if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
+
+    const size_t N = (size_t)std::max(p->N, 1), BN = (size_t)B * N;
+    std::vector<rl::SegRec> segs;
+    make_segrecs(prob->inner_seg, prob->Ei, segs);
+    make_segrecs(prob->outer_seg, prob->Eo, segs);
+    if ((rc = p->alloc(&p->d_center, 2 * N)) || (rc = p->alloc(&p->d_seg, segs.size())) ||
+        (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
+        return cleanup(rc);
+    hipStream_t st = p->own_stream;
+    if (p->N > 0 && hipMemcpyAsync(p->d_center, prob->center_xy, 2 * N * sizeof(double), hipMemcpyHostToDevice, st))
+        return cleanup(fail(RL_EHIP, "upload center"));
+    if (!segs.empty() && hipMemcpyAsync(p->d_seg, segs.data(), segs.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st))
+        return cleanup(fail(RL_EHIP, "upload segments"));
+    if (hipMemcpyAsync(p->d_cfg, cfg, (size_t)n_cfg * sizeof(rl_cfg), hipMemcpyHostToDevice, st))
+        return cleanup(fail(RL_EHIP, "upload cfg"));
+    std::vector<uint64_t> sd((size_t)B, 0);
+    if (seeds) std::memcpy(sd.data(), seeds, (size_t)B * sizeof(uint64_t));
+    if (hipMemcpyAsync(p->d_seeds, sd.data(), (size_t)B * sizeof(uint64_t), hipMemcpyHostToDevice, st))
+        return cleanup(fail(RL_EHIP, "upload seeds"));
+    for (int m = 0; m < 2; ++m) {
+        if (!(modes & (1 << m))) continue;
+        ModeBufs& mb = p->mb[m];
+        if ((rc = p->alloc(&mb.x, BN)) || (rc = p->alloc(&mb.y, BN)) || (rc = p->alloc(&mb.heading, BN)) ||
+            (rc = p->alloc(&mb.kappa, BN)) || (rc = p->alloc(&mb.alpha_total, BN)) ||
+            (rc = p->alloc(&mb.alpha_last, BN)) || (rc = p->alloc(&mb.nx, BN)) || (rc = p->alloc(&mb.ny, BN)) ||
+            (rc = p->alloc(&mb.evals, (size_t)B * std::max(mo, 1))) ||
+            (rc = p->alloc(&mb.accepts, (size_t)B * std::max(mo, 1))))
+            return cleanup(rc);
+        if (m == 1) {
+            if ((rc = p->alloc(&mb.v, BN)) || (rc = p->alloc(&mb.ax, BN)) || (rc = p->alloc(&mb.lap, (size_t)B)) ||
+                (rc = p->alloc(&mb.sweeps, (size_t)B * (mo + 1))))
+                return cleanup(rc);
+        }
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(RL_EHIP, "upload sync"));
+    *out = p;
+    return RL_OK;
+}
+
+int rl_plan_run(rl_plan* p, void* hip_stream) {
+    if (!p) return fail(RL_EINVAL, "plan is NULL");
+    HIPCHK(hipSetDevice(p->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : p->own_stream;
+    p->last_stream = st;
+    HIPCHK(hipEventRecord(p->ev[0], st));
+    for (int m = 0; m < 2; ++m) {
+        if (!(p->modes & (1 << m))) continue;
+        ModeBufs& mb = p->mb[m];
+        const size_t BN = (size_t)p->B * (size_t)std::max(p->N, 1);
+        if (p->N == 0 || p->max_outer == 0) {
+            // ref:689 / 912 — N==0 returns an empty Result; zero the counters
+            HIPCHK(hipMemsetAsync(mb.evals, 0, sizeof(int32_t) * p->B * std::max(p->max_outer, 1), st));
+            HIPCHK(hipMemsetAsync(mb.accepts, 0, sizeof(int32_t) * p->B * std::max(p->max_outer, 1), st));
+            if (m == 1) {
+                HIPCHK(hipMemsetAsync(mb.lap, 0, sizeof(double) * p->B, st));
+                HIPCHK(hipMemsetAsync(mb.sweeps, 0, sizeof(int32_t) * p->B * (p->max_outer + 1), st));
+            }
+            if (p->N == 0) continue;
+        }
+        (void)BN;
+        rl::KParams kp;
+        kp.center = p->d_center;
+        kp.seg = p->d_seg;
+        kp.cfg = p->d_cfg;
+        kp.seeds = p->d_seeds;
+        kp.x = mb.x; kp.y = mb.y; kp.heading = mb.heading; kp.kappa = mb.kappa;
+        kp.alpha_total = mb.alpha_total; kp.alpha_last = mb.alpha_last;
+        kp.v = mb.v; kp.ax = mb.ax; kp.lap = mb.lap; kp.nx = mb.nx; kp.ny = mb.ny;
+        kp.evals = mb.evals; kp.accepts = mb.accepts; kp.sweeps = mb.sweeps;
+        kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
+        kp.L = p->L; kp.veh_width = p->veh_width;
+        HIPCHK(hipEventRecord(p->ev[1 + m], st));
+        hipError_t e = rl::launch_optimize(kp, m == 1, st);
+        if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    }
+    HIPCHK(hipEventRecord(p->ev[3], st));
+    p->ran = true;
+    return RL_OK;
+}
+
+int rl_plan_kernel_ms(rl_plan* p, int32_t idx, float* ms) {
+    if (!p || !ms || !p->ran) return fail(RL_EINVAL, "plan not run");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipEventSynchronize(p->ev[3]));
+    // idx 0: whole run; 1: min-curv kernel; 2: min-time kernel
+    hipEvent_t a, b;
+    const bool mc = p->modes & RL_MODE_MINCURV, mt = p->modes & RL_MODE_MINTIME;
+    if (idx == 0) { a = p->ev[0]; b = p->ev[3]; }
+    else if (idx == 1 && mc) { a = p->ev[1]; b = mt ? p->ev[2] : p->ev[3]; }
+    else if (idx == 2 && mt) { a = p->ev[2]; b = p->ev[3]; }
+    else return fail(RL_EINVAL, "kernel index not in this plan");
+    HIPCHK(hipEventElapsedTime(ms, a, b));
+    return RL_OK;
+}
+
+static int fetch_mode(rl_plan* p, int m, rl_out* o, hipStream_t st) {
+    if (!o) return RL_OK;
+    ModeBufs& mb = p->mb[m];
+    const size_t BN = (size_t)p->B * (size_t)p->N;
+    auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
+        if (!dst || !src || bytes == 0) return RL_OK;
+        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+        return e == hipSuccess ? RL_OK : fail(RL_EHIP, std::string("download: ") + hipGetErrorString(e));
+    };
+    int rc;
+    if ((rc = cp(o->x, mb.x, BN * 8)) || (rc = cp(o->y, mb.y, BN * 8)) || (rc = cp(o->heading, mb.heading, BN * 8)) ||
+        (rc = cp(o->kappa, mb.kappa, BN * 8)) || (rc = cp(o->alpha_total, mb.alpha_total, BN * 8)) ||
+        (rc = cp(o->alpha_last, mb.alpha_last, BN * 8)) ||
+        (rc = cp(o->evals, mb.evals, (size_t)p->B * p->max_outer * 4)) ||
+        (rc = cp(o->accepts, mb.accepts, (size_t)p->B * p->max_outer * 4)))
+        return rc;
+    if (m == 1) {
+        if ((rc = cp(o->v, mb.v, BN * 8)) || (rc = cp(o->ax, mb.ax, BN * 8)) || (rc = cp(o->lap, mb.lap, (size_t)p->B * 8)) ||
+            (rc = cp(o->vpass_sweeps, mb.sweeps, (size_t)p->B * (p->max_outer + 1) * 4)))
+            return rc;
+    }
+    return RL_OK;
+}
+
+int rl_plan_fetch(rl_plan* p, rl_out* out_mc, rl_out* out_mt) {
+    if (!p) return fail(RL_EINVAL, "plan is NULL");
+    if ((out_mc && !(p->modes & RL_MODE_MINCURV)) || (out_mt && !(p->modes & RL_MODE_MINTIME)))
+        return fail(RL_EINVAL, "requested a mode the plan did not run");
+    HIPCHK(hipSetDevice(p->device));
+    hipStream_t st = p->last_stream ? p->last_stream : p->own_stream;
+    int rc;
+    if ((rc = fetch_mode(p, 0, out_mc, st)) || (rc = fetch_mode(p, 1, out_mt, st))) return rc;
+    HIPCHK(hipStreamSynchronize(st));
+    return RL_OK;
+}
+
+int rl_plan_device_outputs(rl_plan* p, int32_t which, rl_out* d) {
+    if (!p || !d) return fail(RL_EINVAL, "NULL argument");
+    int m = (which == RL_MODE_MINCURV) ? 0 : (which == RL_MODE_MINTIME ? 1 : -1);
+    if (m < 0 || !(p->modes & which)) return fail(RL_EINVAL, "mode not in plan");
+    ModeBufs& mb = p->mb[m];
+    std::memset(d, 0, sizeof(*d));
+    d->x = mb.x; d->y = mb.y; d->heading = mb.heading; d->kappa = mb.kappa;
+    d->alpha_total = mb.alpha_total; d->alpha_last = mb.alpha_last;
+    d->v = mb.v; d->ax = mb.ax; d->lap = mb.lap;
+    d->evals = mb.evals; d->accepts = mb.accepts; d->vpass_sweeps = mb.sweeps;
+    return RL_OK;
+}
+
+int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
+                rl_out* out_mincurv, rl_out* out_mintime) {
+    int modes = (out_mincurv ? RL_MODE_MINCURV : 0) | (out_mintime ? RL_MODE_MINTIME : 0);
+    if (!modes) return fail(RL_EINVAL, "no output requested");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    rl_plan* p = nullptr;
+    int rc = rl_plan_create(&p, dev, prob, cfg, n_cfg, seeds, B, modes);
+    if (rc) return rc;
+    rc = rl_plan_run(p, nullptr);
+    if (!rc) rc = rl_plan_fetch(p, out_mincurv, out_mintime);
+    rl_plan_destroy(p);
+    return rc;
+}
+
+}  // extern "C"

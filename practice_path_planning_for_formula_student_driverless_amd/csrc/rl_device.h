@@ -1,0 +1,71 @@
+// rl_device.h — device-side math shared by the raceline kernels (gfx950, fp64).
+//
+// Every helper restates one reference expression (ref = /root/reference/src/main.cpp)
+// with the same operations in the same order; the translation unit is compiled
+// with -ffp-contract=off so no a*b+c is fused.  f64 +,-,*,/ and sqrt are
+// correctly rounded on gfx950 (div_scale/div_fmas/div_fixup and the
+// Newton-refined rsq sequence), so they reproduce the CPU bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rl {
+
+// libstdc++ std::max / std::min / std::clamp comparison forms (NaN behaviour included)
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double sclamp(double v, double lo, double hi) { return (v < lo) ? lo : ((hi < v) ? hi : v); }
+
+// SURVEY.md §8d α-seed: splitmix64(seed, counter=i) -> U(-1,1), seed 0 -> 0
+__host__ __device__ __forceinline__ double seed_value(uint64_t seed, int32_t i, double sigma) {
+    if (seed == 0) return 0.0;
+    uint64_t z = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    double u = (double)(z >> 11) * 0x1.0p-53;
+    return sigma * (2.0 * u - 1.0);
+}
+
+// Segment record prepared on the host from a reference segment pair (S0,S1):
+//   vx,vy = S1-S0             (rayIntersectSegment ref:482; minDistance ab ref:505)
+//   denom = max(1e-30, |ab|^2) (ref:506)
+//   mx,my,hr = midpoint and half-length(+slack) for conservative culling
+struct SegRec {
+    double x0, y0, vx, vy, denom, mx, my, hr;
+};
+static_assert(sizeof(SegRec) == 64, "SegRec must be 64 B");
+
+// Derived v-pass constants, evaluated exactly as the reference expressions
+// of ax_max_at (ref:797-824) evaluate their constant prefixes.
+struct VConst {
+    double a_total;     // use_total_ge_lat ? max(a_total_max, a_lat_max) : a_total_max
+    double a_total2;    // a_total*a_total
+    double kFd;         // (0.5*rho_air)*Cd*A_front_m2
+    double Fr;          // mass_kg*9.81*c_rr
+    double mass, Pmax, acc_cap, brk_cap;
+    double h, two_h;
+};
+
+// forward step of velocity_profile_forward_backward (ref:829-833):
+//   a_acc = ax_max_at(v,k).first ; return sqrt(max(0, v*v + 2*a_acc*h))
+__device__ __forceinline__ double vstep_fwd(const VConst& c, double vi, double ki) {
+    double alat = vi * vi * fabs(ki);
+    double a_res = sqrt(smax(0.0, c.a_total2 - alat * alat));
+    double Fd = c.kFd * vi * vi;
+    double a_power = (c.Pmax > 0 && vi > 1e-6) ? (c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass) : 1e9;
+    double a_acc = smin(smin(a_res, c.acc_cap), a_power);
+    a_acc = smax(0.0, a_acc);
+    return sqrt(smax(0.0, vi * vi + 2.0 * a_acc * c.h));
+}
+// backward step (ref:841-845): a_brk = ax_max_at(v,k).second
+__device__ __forceinline__ double vstep_bwd(const VConst& c, double vi, double ki) {
+    double alat = vi * vi * fabs(ki);
+    double a_res = sqrt(smax(0.0, c.a_total2 - alat * alat));
+    double Fd = c.kFd * vi * vi;
+    double a_brk = smin(a_res, c.brk_cap) + (Fd + c.Fr) / c.mass;
+    a_brk = smax(0.0, a_brk);
+    return sqrt(smax(0.0, vi * vi + 2.0 * a_brk * c.h));
+}
+
+}  // namespace rl

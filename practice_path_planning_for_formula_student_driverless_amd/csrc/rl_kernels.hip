@@ -1,0 +1,781 @@
+// rl_kernels.hip — MI355X (gfx950) batched raceline optimizer: steps 7-8 of the
+// reference pipeline (ref = /root/reference/src/main.cpp) as one persistent
+// kernel per (problem, mode).
+//
+// Mapping:
+//   * one workgroup = one track instance (α-seed / cfg sweep point); the whole
+//     optimiser (max_outer_iters linearisations x PGD/Armijo inner loop x
+//     corridor updates, and for min-time the v(s) passes) runs in one launch;
+//   * thread t owns K contiguous samples [t*K, t*K+K).  The mutable inner-loop
+//     state (α, grad, α_trial, lo, hi, q1, q2, D1α[, γ²]) lives in VGPRs; the
+//     read-only linearisation (A1,A2 | N0,W) is staged once per outer
+//     iteration in LDS as [pair][k][t] double2 (lane-consecutive 16-B reads,
+//     bank-conflict free, each thread reads only its own entries);
+//   * the tridiagonal stencils need one neighbour on each side: chunk edges
+//     move lane-to-lane with DPP wave_shr/wave_shl and across waves through a
+//     per-wave LDS edge table; an evaluation costs two workgroup barriers;
+//   * J, Jsm and the Armijo decrease are reduced per wave then across waves in
+//     a fixed order, so the accept/backtrack decision is uniform;
+//   * outer-level state (P, n, α_total, α_last) lives in the instance's slice of
+//     the result arrays in HBM and is touched once per outer iteration;
+//   * the serial v(s) recurrence runs as an exact chunked relaxation: every
+//     thread recomputes its chunk from the pass-start values with the value its
+//     neighbour published, until no published value changes; the fixed point
+//     is the serial result bit for bit.
+// All arithmetic is IEEE fp64 (-ffp-contract=off).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_abi.h"
+#include "rl_device.h"
+#include "rl_kernels.h"
+#include "rl_math.h"
+
+#define RL_AI __attribute__((always_inline))
+
+namespace rl {
+
+constexpr int CK = 4;   // corridor sub-chunk (samples per ray-scan pass)
+
+// ------------------------------------------------------------ wave primitives
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+// lane l <- lane l-1 (DPP wave_shr:1); lane 0 gets 0
+__device__ __forceinline__ double dpp_from_left(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+// lane l <- lane l+1 (DPP wave_shl:1); lane 63 gets 0
+__device__ __forceinline__ double dpp_from_right(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+// keep v opaque to loop-invariant code motion (stops hoisting of per-sample addresses)
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// a[idx] for a runtime idx as a bit-mask blend: a select chain would be turned
+// into an indexed load, which forces the whole array out of VGPRs into scratch
+template <int K>
+__device__ __forceinline__ double pick(const double (&a)[K], int idx) {
+    unsigned long long r = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const unsigned long long m = 0ull - (unsigned long long)(k == idx);
+        r |= (unsigned long long)__double_as_longlong(a[k]) & m;
+    }
+    return __longlong_as_double((long long)r);
+}
+template <int K>
+__device__ __forceinline__ void put(double (&a)[K], int idx, double v) {
+    const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const unsigned long long m = 0ull - (unsigned long long)(k == idx);
+        const unsigned long long ab = (unsigned long long)__double_as_longlong(a[k]);
+        a[k] = __longlong_as_double((long long)((ab & ~m) | (vb & m)));
+    }
+}
+
+template <int K, int T>
+struct alignas(16) Smem {
+    static constexpr int NW = T / 64;
+    union {
+        double2 coef[2][K][T];   // [0]: (A1,A2)  [1]: (N0,W)   (precompute_lin_geom_generic)
+        double vin[2][T];        // v-pass relaxation: published outgoing values
+    } u;
+    double eF[4][NW];            // per exchange slot: lane-0 first value of each wave
+    double eL[4][NW];            //                    lane-63 last value of each wave
+    double wL[4];                // last valid value of the last active thread (closed wrap)
+    double red[3][NW];           // per-wave partial sums of an evaluation
+    double red2[2][NW];          // other block reductions
+    double bc[4];                // broadcast scalars
+};
+
+// --------------------------------------------------------------- the kernel
+// waves per SIMD to keep resident (caps the register budget the compiler may use)
+template <int T>
+struct MinWaves { static constexpr int value = (T >= 512) ? 1 : (T == 64 ? 4 : 2); };
+
+template <int K, int T, bool CLOSED, bool MT>
+__global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KParams p) {
+    constexpr int NW = T / 64;
+    __shared__ Smem<K, T> sm;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int b = blockIdx.x;
+    const int N = p.N;
+    const int base = tid * K;
+    const int cnt = min(K, max(0, N - base));
+    const int Ta = (N + K - 1) / K;
+    const bool active = tid < Ta;
+    const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
+    const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
+
+    const double h = p.L / (double)N;                    // ref:690 / 913
+    const double invh = 1.0 / h, inv2h = 1.0 / (2 * h), invh2 = 1.0 / (h * h);   // ref:547, 562
+    const double m2invh2 = -2 * invh2;                   // ref:577 (-2*invh2)
+    const double two_h = 2 * h, hh = h * h;              // ref:602-603 divisors
+    const double lam = C.lambda_smooth;
+    const double lam2 = 2.0 * lam;                       // ref:673 2.0*lambda_smooth*gsm
+
+    const size_t off = (size_t)b * (size_t)N;
+    double* __restrict__ X = p.x + off;                  // P.x (state, then output)
+    double* __restrict__ Y = p.y + off;
+    double* __restrict__ NX = p.nx + off;                // normals (scratch)
+    double* __restrict__ NY = p.ny + off;
+    double* __restrict__ ATOT = p.alpha_total + off;
+    double* __restrict__ ALAST = p.alpha_last + off;
+
+    // ---- neighbour exchange (DPP in-wave, LDS across waves and for the wrap) ----
+    // before a barrier: dl/dr receive the in-wave neighbour values
+    auto xpub = [&](int slot, const double (&a)[K], double& dl, double& dr) RL_AI {
+        const double first = a[0], last = a[K - 1];
+        dl = dpp_from_left(last);
+        dr = dpp_from_right(first);
+        if (lane == 0) sm.eF[slot][wid] = first;
+        if (lane == 63) sm.eL[slot][wid] = last;
+        if (tid == Ta - 1) sm.wL[slot] = (cnt == K) ? last : pick(a, cnt - 1);
+    };
+    // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped)
+    auto xget = [&](int slot, double dl, double dr, double& lv, double& rv) RL_AI {
+        lv = dl;
+        if (lane == 0) lv = (wid > 0) ? sm.eL[slot][wid - 1] : sm.wL[slot];
+        rv = dr;
+        if (lane == 63 && wid + 1 < NW) rv = sm.eF[slot][wid + 1];
+        if (tid == Ta - 1) rv = sm.eF[slot][0];
+    };
+    // the last active thread's padding slots take the right neighbour, so every
+    // stencil reads a[k+1] (k<K-1) or rv (k=K-1) uniformly
+    auto fill_pad = [&](double (&a)[K], double rv) RL_AI {
+        if (cnt != K) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) a[k] = (k < cnt) ? a[k] : rv;
+        }
+    };
+
+    // ---- P-neighbourhood helpers --------------------------------------------
+    // P with a halo of 2 on each side: px[j] = P[base-2+j] (wrapped / clamped)
+    auto loadP = [&](double (&px)[K + 4], double (&py)[K + 4]) RL_AI {
+        const int bs = opaque(base);
+        if (bs >= 2 && bs + K + 2 <= N) {
+            const double* xb = X + (bs - 2);
+            const double* yb = Y + (bs - 2);
+#pragma unroll
+            for (int j = 0; j < K + 4; ++j) { px[j] = xb[j]; py[j] = yb[j]; }
+        } else {
+#pragma unroll
+            for (int j = 0; j < K + 4; ++j) {
+                int g = bs - 2 + j;
+                if (CLOSED) { g %= N; if (g < 0) g += N; }
+                else g = g < 0 ? 0 : (g >= N ? N - 1 : g);
+                px[j] = X[g];
+                py[j] = Y[g];
+            }
+        }
+    };
+    // own sample k (clamped for padding)
+    auto own = [&](int k) RL_AI -> int { return min(opaque(base) + k, N - 1); };
+    // the `deriv` lambdas of ref:599-613 / 625-639 for own sample k (P index k+2)
+    auto deriv = [&](const double (&px)[K + 4], const double (&py)[K + 4], int k, double& xp, double& yp,
+                     double& xpp, double& ypp) RL_AI {
+        const int i = base + k;
+        if (N == 1) { xp = 1; yp = 0; xpp = ypp = 0; return; }
+        if (CLOSED) {
+            xp = (px[k + 3] - px[k + 1]) / two_h; yp = (py[k + 3] - py[k + 1]) / two_h;
+            xpp = (px[k + 3] - 2 * px[k + 2] + px[k + 1]) / hh; ypp = (py[k + 3] - 2 * py[k + 2] + py[k + 1]) / hh;
+        } else if (i == 0) {
+            xp = (px[k + 3] - px[k + 2]) / h; yp = (py[k + 3] - py[k + 2]) / h;
+            if (N >= 3) { xpp = (px[k + 4] - 2 * px[k + 3] + px[k + 2]) / hh; ypp = (py[k + 4] - 2 * py[k + 3] + py[k + 2]) / hh; }
+            else xpp = ypp = 0;
+        } else if (i == N - 1) {
+            xp = (px[k + 2] - px[k + 1]) / h; yp = (py[k + 2] - py[k + 1]) / h;
+            if (N >= 3) { xpp = (px[k + 2] - 2 * px[k + 1] + px[k]) / hh; ypp = (py[k + 2] - 2 * py[k + 1] + py[k]) / hh; }
+            else xpp = ypp = 0;
+        } else {
+            xp = (px[k + 3] - px[k + 1]) / two_h; yp = (py[k + 3] - py[k + 1]) / two_h;
+            xpp = (px[k + 3] - 2 * px[k + 2] + px[k + 1]) / hh; ypp = (py[k + 3] - 2 * py[k + 2] + py[k + 1]) / hh;
+        }
+    };
+    // normals_from_points_generic ref:581-593, own valid samples -> NX/NY
+    auto normals = [&]() RL_AI {
+        if (!active) return;
+        double px[K + 4], py[K + 4];
+        loadP(px, py);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = base + k;
+            double tx, ty;
+            if (N == 1) { tx = 1; ty = 0; }
+            else if (CLOSED) { tx = (px[k + 3] - px[k + 1]) * 0.5; ty = (py[k + 3] - py[k + 1]) * 0.5; }
+            else if (i == 0) { tx = px[k + 3] - px[k + 2]; ty = py[k + 3] - py[k + 2]; }
+            else if (i == N - 1) { tx = px[k + 2] - px[k + 1]; ty = py[k + 2] - py[k + 1]; }
+            else { tx = (px[k + 3] - px[k + 1]) * 0.5; ty = (py[k + 3] - py[k + 1]) * 0.5; }
+            if (sqrt(tx * tx + ty * ty) < 1e-15) { tx = 1; ty = 0; }
+            double vx = -ty, vy = tx;
+            double n = sqrt(vx * vx + vy * vy);              // geom::normalize ref:132
+            double ox = 0, oy = 0;
+            if (!(n < 1e-15)) { ox = vx / n; oy = vy / n; }
+            if (k < cnt) { NX[i] = ox; NY[i] = oy; }
+        }
+    };
+    // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin), CK samples at a time
+    auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
+        const SegRec* __restrict__ S = p.seg;
+        const int Ei = p.Ei, Ee = p.Ei + p.Eo;
+#pragma unroll
+        for (int c = 0; c < K; c += CK) {
+            double qx[CK], qy[CK], ux[CK], uy[CK];
+            double bpi[CK], bni[CK], bpo[CK], bno[CK];
+#pragma unroll
+            for (int k = 0; k < CK; ++k) {
+                const int i = own(c + k);
+                qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
+                bpi[k] = bni[k] = bpo[k] = bno[k] = INFINITY;
+            }
+            // rayToRingDistance ref:491-500 over rayIntersectSegment ref:478-490, both
+            // directions at once: dir=-n gives den'=-den, t'=-t, u'=u bit-exactly
+            auto scan = [&](int e0, int e1, double (&bp)[CK], double (&bn)[CK]) RL_AI {
+                for (int e = e0; e < e1; ++e) {
+                    const SegRec s = S[e];
+#pragma unroll
+                    for (int k = 0; k < CK; ++k) {
+                        double den = ux[k] * (-s.vy) + uy[k] * (s.vx);
+                        if (fabs(den) < 1e-15) continue;
+                        double ax = s.x0 - qx[k], ay = s.y0 - qy[k];
+                        double inv = 1.0 / den;
+                        double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
+                        double u = (ux[k] * ay - uy[k] * ax) * inv;
+                        if (u >= -1e-12 && u <= 1.0 + 1e-12) {
+                            if (t > 0.0 && t < bp[k]) bp[k] = t;
+                            double tn = -t;
+                            if (tn > 0.0 && tn < bn[k]) bn[k] = tn;
+                        }
+                    }
+                }
+            };
+            scan(0, Ei, bpi, bni);
+            scan(Ei, Ee, bpo, bno);
+            // minDistanceToSegments_global fallback (ref:501-512) where a ray missed
+            auto mindist = [&](int e0, int e1, double (&md)[CK]) RL_AI {
+                for (int e = e0; e < e1; ++e) {
+                    const SegRec s = S[e];
+#pragma unroll
+                    for (int k = 0; k < CK; ++k) {
+                        double apx = qx[k] - s.x0, apy = qy[k] - s.y0;
+                        double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
+                        double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
+                        md[k] = smin(md[k], hypot_ref(qx[k] - Qx, qy[k] - Qy));
+                    }
+                }
+            };
+            bool need_i = false, need_o = false;
+#pragma unroll
+            for (int k = 0; k < CK; ++k) {
+                if (c + k < cnt) {
+                    need_i |= !isfinite(bpi[k]) || !isfinite(bni[k]);
+                    need_o |= !isfinite(bpo[k]) || !isfinite(bno[k]);
+                }
+            }
+            double mdi[CK], mdo[CK];
+#pragma unroll
+            for (int k = 0; k < CK; ++k) mdi[k] = mdo[k] = INFINITY;
+            if (__any(need_i)) mindist(0, Ei, mdi);
+            if (__any(need_o)) mindist(Ei, Ee, mdo);
+#pragma unroll
+            for (int k = 0; k < CK; ++k) {
+                // safe_ray ref:694-699
+                double spi = bpi[k], sni = bni[k], spo = bpo[k], sno = bno[k];
+                if (!isfinite(spi)) spi = mdi[k];
+                if (!isfinite(spi)) spi = 0.0;
+                if (!isfinite(sni)) sni = mdi[k];
+                if (!isfinite(sni)) sni = 0.0;
+                if (!isfinite(spo)) spo = mdo[k];
+                if (!isfinite(spo)) spo = 0.0;
+                if (!isfinite(sno)) sno = mdo[k];
+                if (!isfinite(sno)) sno = 0.0;
+                double dpos = smin(smax(0.0, spi), smax(0.0, spo));
+                double dneg = smin(smax(0.0, sni), smax(0.0, sno));
+                double hk = smax(0.0, dpos - guard);
+                double lk = -smax(0.0, dneg - guard);
+                if (!isfinite(hk)) hk = 0.0;
+                if (!isfinite(lk)) lk = 0.0;
+                hi[c + k] = (c + k < cnt) ? hk : 0.0;
+                lo[c + k] = (c + k < cnt) ? lk : 0.0;
+            }
+        }
+    };
+
+    // ---- v(s) profile: velocity_profile_forward_backward ref:782-862 ---------
+    VConst vc;
+    vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;   // ref:802-804
+    vc.a_total2 = vc.a_total * vc.a_total;
+    vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;     // ref:810 constant prefix
+    vc.Fr = C.mass_kg * 9.81 * C.c_rr;                   // ref:811
+    vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
+    vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
+    vc.h = h; vc.two_h = 2.0 * h;
+
+    // returns sweeps executed; padding samples hold ka=0, v=+inf (never bind)
+    auto vpass = [&](const double (&ka)[K], double (&v)[K]) RL_AI -> int {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double kk = fabs(ka[k]);
+            double v_kappa = sqrt(C.a_lat_max / smax(kk, C.kappa_eps));
+            v[k] = (k < cnt) ? smin(C.v_cap_mps, v_kappa) : INFINITY;   // ref:787-794
+        }
+        const int iters = C.max_vpass_iters;
+        int sweeps = 0;
+        const bool has_right = active && (base + cnt < N);   // chunk feeds a right neighbour
+        const bool has_left = active && (base > 0);
+        for (int s = 0; s < iters; ++s) {
+            ++sweeps;
+            double vstart[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) vstart[k] = v[k];
+            // ---- forward pass (ref:829-833)
+            {
+                double in_prev = -1.0;       // sentinel (valid values are >= 0 or +inf)
+                for (int it = 0;; ++it) {
+                    double in = INFINITY;    // first iteration: no incoming constraint
+                    if (it > 0 && has_left) in = sm.u.vin[(it - 1) & 1][tid - 1];
+                    bool changed = false;
+                    if (active && in != in_prev) {
+                        changed = (it > 0);
+                        in_prev = in;
+                        double cur = vstart[0];
+                        if (has_left) cur = smin(vstart[0], in);     // v[i+1] = min(v[i+1], vf)
+                        v[0] = cur;
+#pragma unroll
+                        for (int k = 0; k + 1 < K; ++k) {
+                            double vf = vstep_fwd(vc, v[k], ka[k]);
+                            v[k + 1] = (k + 1 < cnt) ? smin(vstart[k + 1], vf) : INFINITY;
+                        }
+                        if (has_right) sm.u.vin[it & 1][tid] = vstep_fwd(vc, v[K - 1], ka[K - 1]);
+                    } else if (active && has_right) {
+                        sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
+                    }
+                    if (!__syncthreads_or(changed) && it > 0) break;
+                }
+            }
+            // closed wrap (ref:834-839): v[0] = min(v[0], f(v[N-1], k[N-1]))
+            if (CLOSED) {
+                if (active && base + cnt == N) {
+                    double vl = (cnt == K) ? v[K - 1] : pick(v, cnt - 1);
+                    double kl = (cnt == K) ? ka[K - 1] : pick(ka, cnt - 1);
+                    sm.bc[0] = vstep_fwd(vc, vl, kl);
+                }
+                __syncthreads();
+                if (tid == 0) v[0] = smin(v[0], sm.bc[0]);
+                __syncthreads();
+            }
+            // ---- backward pass (ref:841-845)
+            {
+                double vpre[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) vpre[k] = v[k];
+                double in_prev = -1.0;
+                for (int it = 0;; ++it) {
+                    double in = INFINITY;
+                    if (it > 0 && has_right) in = sm.u.vin[(it - 1) & 1][tid + 1];
+                    bool changed = false;
+                    if (active && in != in_prev) {
+                        changed = (it > 0);
+                        in_prev = in;
+                        // has_right => full chunk (only the last thread can be partial)
+                        v[K - 1] = has_right ? smin(vpre[K - 1], in) : vpre[K - 1];
+#pragma unroll
+                        for (int k = K - 2; k >= 0; --k) {
+                            double vb = vstep_bwd(vc, v[k + 1], ka[k + 1]);
+                            v[k] = (k < cnt) ? smin(vpre[k], vb) : INFINITY;
+                        }
+                        if (has_left) sm.u.vin[it & 1][tid] = vstep_bwd(vc, v[0], ka[0]);
+                    } else if (active && has_left) {
+                        sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
+                    }
+                    if (!__syncthreads_or(changed) && it > 0) break;
+                }
+            }
+            // closed wrap (ref:846-850): v[N-1] = min(v[N-1], b(v[0], k[0]))
+            if (CLOSED) {
+                if (tid == 0) sm.bc[1] = vstep_bwd(vc, v[0], ka[0]);
+                __syncthreads();
+                if (active && base + cnt == N) {
+                    if (cnt == K) v[K - 1] = smin(v[K - 1], sm.bc[1]);
+                    else put(v, cnt - 1, smin(pick(v, cnt - 1), sm.bc[1]));
+                }
+                __syncthreads();
+            }
+            bool any_change = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) any_change |= (k < cnt) && (v[k] != vstart[k]);
+            if (!__syncthreads_or(any_change)) break;   // later sweeps are exact repeats
+        }
+        return sweeps;
+    };
+
+    // ---- difference operators (DiffOps / DiffOpsOpen ref:545-579) -------------
+    auto d1_at = [&](int k, double am, double a0, double ap) RL_AI -> double {   // D1 ref:549-551 / 563-566
+        if (CLOSED) return (ap - am) * inv2h;
+        const int i = base + k;
+        if (N == 1) return 0.0;
+        if (i == 0) return (ap - a0) * invh;
+        if (i == N - 1) return (a0 - am) * invh;
+        return (ap - am) * inv2h;
+    };
+    auto d2_at = [&](int k, double am, double a0, double ap) RL_AI -> double {   // D2 ref:552-554 / 573-575
+        if (CLOSED) return (ap - 2 * a0 + am) * invh2;
+        const int i = base + k;
+        if (N <= 2 || i == 0 || i == N - 1) return 0.0;
+        return (ap - 2 * a0 + am) * invh2;
+    };
+    auto d1t_at = [&](int k, double vm, double v0, double vp) RL_AI -> double {  // D1T ref:555-557 / 567-572
+        if (CLOSED) return (vm - vp) * inv2h;
+        const int j = base + k;
+        if (N <= 1) return 0.0;
+        double acc = 0.0;     // the scatter order of ref:569-571 restated as a gather
+        if (j >= 1) acc += ((j == 1) ? invh : inv2h) * vm;
+        if (j == 0) acc += (-invh) * v0;
+        else if (j == N - 1) acc += (+invh) * v0;
+        if (j <= N - 2) acc += ((j + 1 == N - 1) ? -invh : -inv2h) * vp;
+        return acc;
+    };
+    auto d2t_at = [&](int k, double vm, double v0, double vp) RL_AI -> double {  // D2T ref:558 / 576-578
+        if (CLOSED) return (vp - 2 * v0 + vm) * invh2;
+        const int j = base + k;
+        if (N <= 2) return 0.0;
+        double acc = 0.0;
+        if (j - 1 >= 1 && j - 1 <= N - 2) acc += (+invh2) * vm;
+        if (j >= 1 && j <= N - 2) acc += m2invh2 * v0;
+        if (j + 1 >= 1 && j + 1 <= N - 2) acc += (+invh2) * vp;
+        return acc;
+    };
+
+    // ---- state ------------------------------------------------------------
+    double G2[K];                                   // γ² (min-time)
+    double lo[K], hi[K], al[K], gr[K], an[K];       // corridor, α, grad, α_trial
+    double q1[K], q2[K], a1v[K];                    // gradient stencil inputs of the last evaluation
+    double dl1, dr1, dl2, dr2, dl3, dr3;            // in-wave neighbours of q1, q2, a1v
+
+    // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
+    // of the trial vector a: J (uniform across the workgroup) and the Armijo
+    // decrease Σ grad*(a-α) (ref:733 / 1009); q1,q2,D1α and their in-wave
+    // neighbours are left for eval_grad.
+    auto eval_j = [&](double (&a)[K], bool trial, double& dec) RL_AI -> double {
+        double pdec = 0.0;
+        if (trial) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k < cnt) pdec += gr[k] * (a[k] - al[k]);
+        }
+        double dl0, dr0;
+        xpub(0, a, dl0, dr0);
+        __syncthreads();
+        double lv, rv;
+        xget(0, dl0, dr0, lv, rv);
+        fill_pad(a, rv);
+        double pJ = 0.0, pJsm = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double2 c01 = sm.u.coef[0][k][tid];   // (A1, A2)
+            const double2 c23 = sm.u.coef[1][k][tid];   // (N0, W)
+            double am = (k > 0) ? a[k - 1] : lv;
+            double ap = (k + 1 < K) ? a[k + 1] : rv;
+            double x1 = d1_at(k, am, a[k], ap);
+            double x2 = d2_at(k, am, a[k], ap);
+            double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
+            double jz = MT ? (G2[k] * r * r) : (r * r);
+            double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
+            q1[k] = c01.x * Wz;
+            q2[k] = c01.y * Wz;
+            a1v[k] = x1;
+            if (k < cnt) { pJ += jz; pJsm += x1 * x1; }
+        }
+        xpub(1, q1, dl1, dr1);
+        xpub(2, q2, dl2, dr2);
+        xpub(3, a1v, dl3, dr3);
+        pJ = wave_sum(pJ);
+        pJsm = wave_sum(pJsm);
+        if (trial) pdec = wave_sum(pdec);
+        if (lane == 0) { sm.red[0][wid] = pJ; sm.red[1][wid] = pJsm; sm.red[2][wid] = pdec; }
+        __syncthreads();
+        double J = sm.red[0][0], Jsm = sm.red[1][0], D = sm.red[2][0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) { J += sm.red[0][w]; Jsm += sm.red[1][w]; D += sm.red[2][w]; }
+        J += lam * Jsm;                                 // ref:666 / 883
+        dec = D;
+        return J;
+    };
+    // gradient of the last evaluation (ref:668-673 / 886-893)
+    auto eval_grad = [&]() RL_AI {
+        double l1, r1, l2, r2, l3, r3;
+        xget(1, dl1, dr1, l1, r1);
+        xget(2, dl2, dr2, l2, r2);
+        xget(3, dl3, dr3, l3, r3);
+        fill_pad(q1, r1);
+        fill_pad(q2, r2);
+        fill_pad(a1v, r3);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double g1 = d1t_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1);
+            double g2 = d2t_at(k, (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2);
+            double gsm = d1t_at(k, (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
+            gr[k] = 2.0 * (g1 + g2) + lam2 * gsm;
+        }
+    };
+
+    // ======================================================================
+    // driver: compute_min_curvature_raceline ref:683-764 /
+    //         compute_min_time_raceline ref:905-1052
+    // ======================================================================
+    if (active) {                                                // P := center
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (k < cnt) {
+                X[base + k] = p.center[2 * (base + k)];
+                Y[base + k] = p.center[2 * (base + k) + 1];
+                ATOT[base + k] = 0.0;
+                ALAST[base + k] = 0.0;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) { al[k] = 0.0; gr[k] = 0.0; G2[k] = 0.0; }
+
+    const int MO = C.max_outer_iters;
+    for (int outer = 0;; ++outer) {
+        if (outer > 0 && active) {
+            // update (ref:743-746 / 1027-1030): alpha_last, P += n*alpha, alpha_accum
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (k < cnt) {
+                    const int i = base + k;
+                    ALAST[i] = al[k];
+                    X[i] += NX[i] * al[k];
+                    Y[i] += NY[i] * al[k];
+                    ATOT[i] += al[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) { al[k] = 0.0; gr[k] = 0.0; }   // ref:757 / 1041
+        __syncthreads();
+        if (outer < MO) {
+            // normals + corridor (ref:692-711 initially with the veh_width argument,
+            // ref:746-756 after each update with cfg veh_width_m)
+            normals();
+            __syncthreads();
+            const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
+            corridor(guard, lo, hi);
+            if (outer == 0 && seed != 0) {                      // ref:720 + seed
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    double s0 = seed_value(seed, base + k, RL_SEED_SIGMA);
+                    al[k] = (k < cnt) ? smin(hi[k], smax(lo[k], s0)) : 0.0;
+                }
+            }
+        }
+        double ka[K];
+        if (MT || outer == MO) {
+            // heading_curv_from_points_generic ref:595-620
+            double hd[K];
+            double px[K + 4], py[K + 4];
+            loadP(px, py);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                double xp, yp, xpp, ypp;
+                deriv(px, py, k, xp, yp, xpp, ypp);
+                double hdv = (outer == MO) ? atan2(yp, xp) : 0.0;   // heading is an output only
+                double denom = pow15(smax(1e-12, xp * xp + yp * yp));
+                double kav = (xp * ypp - yp * xpp) / denom;
+                hd[k] = (k < cnt) ? hdv : 0.0;
+                ka[k] = (k < cnt) ? kav : 0.0;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (outer == MO && active) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (k < cnt) { p.heading[off + base + k] = hd[k]; p.kappa[off + base + k] = ka[k]; }
+            }
+        }
+        if (MT) {
+            double v[K];
+            int sw = vpass(ka, v);                               // ref:947 / 1047
+            if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
+            if (outer == MO) {
+                // ax and lap time (ref:854-860)
+                double dl, dr, lv, rv;
+                xpub(0, v, dl, dr);
+                __syncthreads();
+                xget(0, dl, dr, lv, rv);
+                double lt = 0.0;
+                if (active) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        if (k < cnt) {
+                            const int i = base + k;
+                            double v1;
+                            if (i + 1 < N) v1 = (k + 1 < cnt) ? v[(k + 1 < K) ? k + 1 : k] : rv;
+                            else v1 = CLOSED ? rv : v[k];
+                            double v0 = v[k];
+                            p.ax[off + i] = (v1 * v1 - v0 * v0) / (2.0 * h);
+                            p.v[off + i] = v0;
+                            lt += h / smax(1e-6, v[k]);
+                        }
+                    }
+                }
+                lt = wave_sum(lt);
+                if (lane == 0) sm.red2[1][wid] = lt;
+                __syncthreads();
+                if (tid == 0 && p.lap) {
+                    double tot = sm.red2[1][0];
+                    for (int w = 1; w < NW; ++w) tot += sm.red2[1][w];
+                    p.lap[b] = tot;
+                }
+            } else {
+                // time weights γ² (ref:950-977)
+                double v_avg = 0.0;
+                if (C.time_weight_use_inv_v) {                   // ref:951 (read only when enabled)
+                    double vs = 0.0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) if (k < cnt) vs += v[k];
+                    vs = wave_sum(vs);
+                    if (lane == 0) sm.red2[0][wid] = vs;
+                    __syncthreads();
+                    double tot = sm.red2[0][0];
+                    for (int w = 1; w < NW; ++w) tot += sm.red2[0][w];
+                    v_avg = tot / (double)(N > 1 ? N : 1);
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    double kk = fabs(ka[k]);
+                    double vkappa = sqrt(C.a_lat_max / smax(kk, C.kappa_eps));
+                    double rr = smin(1.0, v[k] / smax(1e-6, vkappa));
+                    double r = rr * rr;                                     // std::pow(.., 2.0)
+                    r = smin(1.0, smax(0.0, r));
+                    double rp;
+                    if (C.time_gamma_power == 2.0) rp = r * r;           // GCC folds pow(r, 2.0) to r*r
+                    else { rp = pow(r, C.time_gamma_power); __builtin_amdgcn_sched_barrier(0); }
+                    double corner_w = 1.0 + C.w_time_gain * rp;
+                    double invv_w = 1.0;
+                    if (C.time_weight_use_inv_v) {
+                        double ratio = v_avg / smax(1e-6, v[k]);
+                        invv_w = 1.0 + C.inv_v_gain * (ratio - 1.0);
+                        if (invv_w < 1.0) invv_w = 1.0;
+                        if (invv_w > 3.0) invv_w = 3.0;
+                    }
+                    double gamma = corner_w * invv_w;
+                    G2[k] = (k < cnt) ? gamma * gamma : 0.0;
+                }
+                __syncthreads();   // vin (aliased with coef) fully consumed before coef is written
+            }
+        }
+        if (outer == MO) break;
+
+        // precompute_lin_geom_generic ref:622-651 -> LDS (own entries only)
+        {
+            double px[K + 4], py[K + 4];
+            loadP(px, py);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                double xp, yp, xpp, ypp;
+                deriv(px, py, k, xp, yp, xpp, ypp);
+                const int i = own(k);
+                double nxk = NX[i], nyk = NY[i];
+                double a1 = nxk * ypp - nyk * xpp;
+                double a2 = xp * nyk - yp * nxk;
+                double n0 = xp * ypp - yp * xpp;
+                double denom = pow15(smax(1e-12, xp * xp + yp * yp));
+                double w = 1.0 / denom;
+                const bool v = k < cnt;
+                sm.u.coef[0][k][tid] = make_double2(v ? a1 : 0.0, v ? a2 : 0.0);
+                sm.u.coef[1][k][tid] = make_double2(v ? n0 : 0.0, v ? w : 0.0);
+            }
+        }
+        // PGD + Armijo (ref:723-742 / 996-1026)
+        double step = C.step_init;
+        double dec;
+        double J = eval_j(al, false, dec);
+        eval_grad();
+        int evals = 1, accepts = 0;
+        double J_prev = J;
+        for (int it = 0; it < C.max_inner_iters; ++it) {
+            bool accepted = false;
+            int bt = 0;
+            while (bt < 20) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    double ai = al[k] - step * gr[k];
+                    an[k] = smin(hi[k], smax(lo[k], ai));
+                }
+                double Jn = eval_j(an, true, dec);
+                ++evals;
+                if (Jn <= J + C.armijo_c * dec) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) al[k] = an[k];
+                    eval_grad();
+                    J = Jn;
+                    accepted = true;
+                    ++accepts;
+                    break;
+                }
+                step *= 0.5;
+                bt++;
+                if (step < C.step_min) break;
+            }
+            if (!accepted) break;
+            if (fabs(J_prev - J) < 1e-10) break;
+            J_prev = J;
+        }
+        if (tid == 0) {
+            if (p.evals) p.evals[(size_t)b * MO + outer] = evals;
+            if (p.accepts) p.accepts[(size_t)b * MO + outer] = accepts;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ launcher
+template <int K, int T, bool CL, bool MT>
+static hipError_t launch_t(const KParams& p, hipStream_t st) {
+    hipLaunchKernelGGL((rl_optimize_kernel<K, T, CL, MT>), dim3(p.B), dim3(T), 0, st, p);
+    return hipGetLastError();
+}
+template <int K, int T>
+static hipError_t launch_kt(const KParams& p, bool mt, hipStream_t st) {
+    if (p.closed) return mt ? launch_t<K, T, true, true>(p, st) : launch_t<K, T, true, false>(p, st);
+    return mt ? launch_t<K, T, false, true>(p, st) : launch_t<K, T, false, false>(p, st);
+}
+
+// variant table: (K, T) by N.  K samples per lane, T lanes per instance.
+int pick_k(int N) {
+    if (N <= 4 * 64) return 4;
+    if (N <= 8 * 512) return 8;
+    return -1;
+}
+static int pick_t(int N) {
+    if (N <= 4 * 64) return 64;
+    if (N <= 8 * 128) return 128;
+    if (N <= 8 * 256) return 256;
+    return 512;
+}
+
+hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
+    if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
+    switch (pick_t(p.N)) {
+        case 64: return launch_kt<4, 64>(p, mintime, st);
+        case 128: return launch_kt<8, 128>(p, mintime, st);
+        case 256: return launch_kt<8, 256>(p, mintime, st);
+        default: return launch_kt<8, 512>(p, mintime, st);
+    }
+}
+
+}  // namespace rl

@@ -1,0 +1,309 @@
+"""Host-side mirror of the reference's raceline interface, over the C-ABI.
+
+Reference (``ref`` = /root/reference/src/main.cpp):
+
+* :func:`compute_min_curvature_raceline` — ``raceline_min_curv::compute_min_curvature_raceline``
+  (ref:683-764): same arguments (center, innerE, outerE, veh_width, L, closed),
+  same :class:`MinCurvResult` fields (raceline, heading, curvature,
+  alpha_total, alpha_last; ref:677-681).
+* :func:`compute_min_time_raceline` — ``raceline_min_time::compute_min_time_raceline``
+  (ref:905-1052), :class:`MinTimeResult` adds v, ax, lap_time (ref:897-903).
+* :func:`ring_edges` / :func:`polyline_edges` — ``edges::ringEdges`` / ``polylineEdges`` (ref:251-260).
+* :func:`compute_raceline_and_save` / :func:`compute_mintime_and_save` — the
+  pipeline callers and their CSV writers (ref:1337-1438), same file names,
+  headers and ``precision(9)`` fixed formatting.
+* ``cfg`` — :func:`default_cfg` holds ``cfg::Config``'s hot-path knobs (ref:77-113).
+
+Beyond the reference: :func:`optimize_batch` and :class:`Plan` run B
+instances (α-seeds, cfg sweeps) in one launch; that is the product.
+
+Every compute call goes through ``librl.so`` (HIP, gfx950).  With no GPU the
+calls raise :class:`RacelineError` (RL_ENODEV): there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .abi import Outputs, Problem, RlCfg, default_cfg, set_mu  # noqa: F401
+
+
+class RacelineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rl error {code}: {msg}")
+        self.code = code
+
+
+def _lib():
+    return abi.load_library()
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RacelineError(rc, _lib().rl_last_error().decode(errors="replace"))
+
+
+# ------------------------------------------------------------------ geometry
+def ring_edges(ring: np.ndarray) -> np.ndarray:
+    """edges::ringEdges (ref:251-255): n segments, the last one closing the ring."""
+    ring = np.ascontiguousarray(ring, dtype=np.float64).reshape(-1, 2)
+    n = len(ring)
+    if n == 0:
+        return np.zeros((0, 4))
+    return np.concatenate([ring, np.roll(ring, -1, axis=0)], axis=1)
+
+
+def polyline_edges(ring: np.ndarray) -> np.ndarray:
+    """edges::polylineEdges (ref:256-260): n-1 segments."""
+    ring = np.ascontiguousarray(ring, dtype=np.float64).reshape(-1, 2)
+    if len(ring) < 2:
+        return np.zeros((0, 4))
+    return np.concatenate([ring[:-1], ring[1:]], axis=1)
+
+
+def edges_for(ring: np.ndarray, closed: bool) -> np.ndarray:
+    return ring_edges(ring) if closed else polyline_edges(ring)
+
+
+# ------------------------------------------------------------------ results
+@dataclass
+class MinCurvResult:
+    """raceline_min_curv::Result (ref:677-681)."""
+
+    raceline: np.ndarray      # [N,2]
+    heading: np.ndarray
+    curvature: np.ndarray
+    alpha_total: np.ndarray
+    alpha_last: np.ndarray
+    evals: Optional[np.ndarray] = None
+
+
+@dataclass
+class MinTimeResult(MinCurvResult):
+    """raceline_min_time::Result (ref:897-903)."""
+
+    v: Optional[np.ndarray] = None
+    ax: Optional[np.ndarray] = None
+    lap_time: float = 0.0
+    vpass_sweeps: Optional[np.ndarray] = None
+
+
+# ------------------------------------------------------------------ batch API
+def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
+                   mincurv: bool = True, mintime: bool = True):
+    """Optimise B instances (seed b / cfg b) of one problem on the GPU.
+
+    cfgs: one RlCfg (broadcast) or a list of B.  seeds: None (all zero — the
+    reference exactly) or B uint64 seeds.  Returns (Outputs|None, Outputs|None).
+    """
+    cfg_arr, ncfg = abi.cfg_array(cfgs)
+    if B is None:
+        B = ncfg if ncfg > 1 else (len(seeds) if seeds is not None else 1)
+    mo = int(cfg_arr[0].max_outer_iters)
+    seeds_a = abi.seed_array(seeds)
+    out_mc = Outputs.alloc(B, prob.N, mo, False) if mincurv else None
+    out_mt = Outputs.alloc(B, prob.N, mo, True) if mintime else None
+    c_mc = out_mc.as_c() if out_mc else None
+    c_mt = out_mt.as_c() if out_mt else None
+    p = prob.as_c()
+    _check(_lib().rl_optimize(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B,
+                              C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None))
+    return out_mc, out_mt
+
+
+class Plan:
+    """Device-resident batch (rl_plan_*): inputs uploaded once, run() enqueues
+    the optimisation on a HIP stream, fetch() copies results to the host."""
+
+    def __init__(self, prob: Problem, cfgs, seeds=None, B: Optional[int] = None, modes: int = abi.RL_MODE_MINCURV,
+                 device: int = 0):
+        cfg_arr, ncfg = abi.cfg_array(cfgs)
+        if B is None:
+            B = ncfg if ncfg > 1 else (len(seeds) if seeds is not None else 1)
+        self.B, self.N, self.modes = B, prob.N, modes
+        self.max_outer = int(cfg_arr[0].max_outer_iters)
+        self._keep = (prob, cfg_arr)
+        seeds_a = abi.seed_array(seeds)
+        h = C.c_void_p()
+        p = prob.as_c()
+        _check(_lib().rl_plan_create(C.byref(h), device, C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B, modes))
+        self._h = h
+
+    def run(self, stream_ptr: int = 0) -> None:
+        _check(_lib().rl_plan_run(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def kernel_ms(self, idx: int) -> float:
+        ms = C.c_float()
+        _check(_lib().rl_plan_kernel_ms(self._h, idx, C.byref(ms)))
+        return float(ms.value)
+
+    def fetch(self):
+        out_mc = Outputs.alloc(self.B, self.N, self.max_outer, False) if self.modes & abi.RL_MODE_MINCURV else None
+        out_mt = Outputs.alloc(self.B, self.N, self.max_outer, True) if self.modes & abi.RL_MODE_MINTIME else None
+        c_mc = out_mc.as_c() if out_mc else None
+        c_mt = out_mt.as_c() if out_mt else None
+        _check(_lib().rl_plan_fetch(self._h, C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None))
+        return out_mc, out_mt
+
+    def device_outputs(self, which: int) -> abi.RlOut:
+        d = abi.RlOut()
+        _check(_lib().rl_plan_device_outputs(self._h, which, C.byref(d)))
+        return d
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib().rl_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# --------------------------------------------------- reference-shaped calls
+def _single(center, innerE, outerE, veh_width, L, closed, cfg, mincurv):
+    cfg = cfg if cfg is not None else default_cfg()
+    prob = Problem(center=center, L=L, inner_seg=innerE, outer_seg=outerE, veh_width=veh_width, closed=closed)
+    if prob.N == 0:                       # ref:689 / 912: N==0 -> empty Result
+        z = np.zeros(0)
+        if mincurv:
+            return MinCurvResult(np.zeros((0, 2)), z, z, z, z)
+        return MinTimeResult(np.zeros((0, 2)), z, z, z, z, v=z, ax=z, lap_time=0.0)
+    mc, mt = optimize_batch(prob, cfg, None, 1, mincurv=mincurv, mintime=not mincurv)
+    o = mc if mincurv else mt
+    res = dict(raceline=np.stack([o.x[0], o.y[0]], axis=1), heading=o.heading[0], curvature=o.kappa[0],
+               alpha_total=o.alpha_total[0], alpha_last=o.alpha_last[0], evals=o.evals[0])
+    if mincurv:
+        return MinCurvResult(**res)
+    return MinTimeResult(**res, v=o.v[0], ax=o.ax[0], lap_time=float(o.lap[0]), vpass_sweeps=o.vpass_sweeps[0])
+
+
+def compute_min_curvature_raceline(center, innerE, outerE, veh_width: float, L: float, closed: bool,
+                                   cfg: Optional[RlCfg] = None) -> MinCurvResult:
+    """raceline_min_curv::compute_min_curvature_raceline (ref:683)."""
+    return _single(center, innerE, outerE, veh_width, L, closed, cfg, True)
+
+
+def compute_min_time_raceline(center, innerE, outerE, veh_width: float, L: float, closed: bool,
+                              cfg: Optional[RlCfg] = None) -> MinTimeResult:
+    """raceline_min_time::compute_min_time_raceline (ref:905)."""
+    return _single(center, innerE, outerE, veh_width, L, closed, cfg, False)
+
+
+# ------------------------------------------------------------- CSV writers
+def _f9(x: float) -> str:
+    """std::fixed + precision(9) (ref:1354)."""
+    return f"{x:.9f}"
+
+
+def _vkappa(kappa: float, cfg: RlCfg) -> float:
+    """v_kappa column (ref:1369-1370): min(v_cap, sqrt(a_lat_max / max(|k|, kappa_eps)))."""
+    k = abs(float(kappa))
+    denom = cfg.kappa_eps if k < cfg.kappa_eps else k          # std::max(|k|, eps)
+    v = float(np.sqrt(cfg.a_lat_max / denom))
+    return cfg.v_cap_mps if v > cfg.v_cap_mps else v
+
+
+def _s_rel(s0: float, L: float, k: int, n: int) -> float:
+    """si - s0 with si = s0 + L*(k/max(1,n)) (ref:1367-1368), same roundings."""
+    return (s0 + L * (float(k) / float(max(1, n)))) - s0
+
+
+def write_raceline_csvs(base: str, res: MinCurvResult, L: float, cfg: Optional[RlCfg] = None,
+                        emit_closed_duplicate: bool = True, s0: float = 0.0) -> None:
+    """Writers of pipeline::compute_raceline_and_save (ref:1351-1382)."""
+    cfg = cfg if cfg is not None else default_cfg()
+    P = res.raceline
+    with open(base + "_raceline.csv", "w") as f:
+        for x, y in P:
+            f.write(f"{_f9(x)},{_f9(y)}\n")
+        if emit_closed_duplicate and len(P):
+            f.write(f"{_f9(P[0, 0])},{_f9(P[0, 1])}\n")
+    with open(base + "_raceline_with_geom.csv", "w") as f:
+        f.write("s,x,y,heading_rad,curvature,alpha_last,v_kappa_mps\n")
+        n = len(P)
+        for k in range(n):
+            s = _s_rel(s0, L, k, n)
+            f.write(",".join(_f9(v) for v in (s, P[k, 0], P[k, 1], res.heading[k], res.curvature[k],
+                                                 res.alpha_last[k], _vkappa(res.curvature[k], cfg))) + "\n")
+        if emit_closed_duplicate and n:
+            f.write(",".join(_f9(v) for v in (L, P[0, 0], P[0, 1], res.heading[0], res.curvature[0],
+                                                 res.alpha_last[0], _vkappa(res.curvature[0], cfg))) + "\n")
+
+
+def write_mintime_csvs(base: str, res: MinTimeResult, L: float, emit_closed_duplicate: bool = True,
+                       s0: float = 0.0) -> None:
+    """Writers of pipeline::compute_mintime_and_save (ref:1400-1436)."""
+    P = res.raceline
+    with open(base + "_mintime_raceline.csv", "w") as f:
+        for x, y in P:
+            f.write(f"{_f9(x)},{_f9(y)}\n")
+        if emit_closed_duplicate and len(P):
+            f.write(f"{_f9(P[0, 0])},{_f9(P[0, 1])}\n")
+    with open(base + "_mintime_with_geom.csv", "w") as f:
+        f.write("s,x,y,heading_rad,curvature,alpha_last,v_mps,ax_mps2\n")
+        n = len(P)
+        for k in range(n):
+            s = _s_rel(s0, L, k, n)
+            f.write(",".join(_f9(v) for v in (s, P[k, 0], P[k, 1], res.heading[k], res.curvature[k],
+                                                 res.alpha_last[k], res.v[k], res.ax[k])) + "\n")
+        if emit_closed_duplicate and n:
+            f.write(",".join(_f9(v) for v in (L, P[0, 0], P[0, 1], res.heading[0], res.curvature[0],
+                                                 res.alpha_last[0], res.v[0], res.ax[0])) + "\n")
+
+
+def compute_raceline_and_save(base: str, center_for_opt, s0: float, L: float, closed: bool, inner_from_mids,
+                              outer_from_mids, cfg: Optional[RlCfg] = None) -> MinCurvResult:
+    """pipeline::compute_raceline_and_save (ref:1337-1383)."""
+    cfg = cfg if cfg is not None else default_cfg()
+    res = compute_min_curvature_raceline(center_for_opt, edges_for(inner_from_mids, closed),
+                                         edges_for(outer_from_mids, closed), cfg.veh_width_m, L, closed, cfg)
+    write_raceline_csvs(base, res, L, cfg, s0=s0)
+    return res
+
+
+def compute_mintime_and_save(base: str, center_for_opt, s0: float, L: float, closed: bool, inner_from_mids,
+                             outer_from_mids, cfg: Optional[RlCfg] = None) -> MinTimeResult:
+    """pipeline::compute_mintime_and_save (ref:1385-1438), without the debug dump."""
+    cfg = cfg if cfg is not None else default_cfg()
+    res = compute_min_time_raceline(center_for_opt, edges_for(inner_from_mids, closed),
+                                    edges_for(outer_from_mids, closed), cfg.veh_width_m, L, closed, cfg)
+    write_mintime_csvs(base, res, L, s0=s0)
+    import sys
+    sys.stderr.write(f"[mintime] Estimated laptime: {res.lap_time:.3f} s\n")
+    return res
+
+
+def load_csv_xy(path: str) -> np.ndarray:
+    """io::loadCSV_XY (ref:267-279): x,y per line; ',' ';' tab or space."""
+    pts = []
+    with open(path) as f:
+        for line in f:
+            if not line.strip():
+                continue
+            parts = line.replace(";", " ").replace("\t", " ").replace(",", " ").split()
+            if len(parts) >= 2:
+                try:
+                    pts.append((float(parts[0]), float(parts[1])))
+                except ValueError:
+                    continue
+    return np.array(pts, dtype=np.float64).reshape(-1, 2)
+
+
+def seeds_range(B: int, first: int = 0) -> np.ndarray:
+    """Seeds first..first+B-1 (seed 0 = the reference's α≡0 start)."""
+    return np.arange(first, first + B, dtype=np.uint64)
+
+
+__all__ = ["RacelineError", "MinCurvResult", "MinTimeResult", "Plan", "Problem", "RlCfg", "Outputs",
+           "default_cfg", "set_mu", "ring_edges", "polyline_edges", "edges_for", "optimize_batch",
+           "compute_min_curvature_raceline", "compute_min_time_raceline", "compute_raceline_and_save",
+           "compute_mintime_and_save", "write_raceline_csvs", "write_mintime_csvs", "load_csv_xy",
+           "seeds_range"]
