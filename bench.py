@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""Benchmark: PGD outer-iterations/s of the batched raceline optimizer on MI355X.
+
+Workload (BASELINE.json configs[1] = SURVEY.md §8d C2): competition_map1 closed,
+N=2000 resample, B=1024 α-seeds per GPU, min-curvature optimiser, default cfg
+(14 outer iterations).  One *step* = one launch optimising the whole batch from
+inputs already resident in HBM; for N>1 the step also gathers the results
+(x, y, κ, α_last, evals) to rank 0 with RCCL over xGMI (the only collective).
+Weak scaling: every rank optimises its own 1024 seeds.
+
+value = (instances x 14 outer iterations, all ranks) / (max over ranks of the
+timed K steps).  Also reported: tracks/s, parity of seed 0 against the
+reference's own fixture, the min-time lap-time Δ (C3 workload, N=2000,
+max_vpass_iters=20) and the single-thread CPU baseline (the C oracle, a bounded
+sample of the same workload) timed on this host.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from practice_path_planning_for_formula_student_driverless_amd import abi, raceline  # noqa: E402
+
+# fp64 peak on MI355X (AMD spec: FP64 vector = FP64 dense matrix = 78.6 TFLOP/s;
+# the path runs on the fp64 VALU, there is no MFMA-shaped contraction in it).
+FP64_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBS = 8000.0
+
+
+def load_problem(name: str):
+    import oracle_lib as O   # fixture loader (npz, no pickle); the oracle itself is not touched here
+
+    case = O.load_case(name)
+    return case, O.case_problem(case), O.case_cfg(case)
+
+
+def flops_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: float = 0.0) -> float:
+    """Algorithmic fp64 flops per outer iteration: +,-,*,/,sqrt each 1.
+    per sample per evaluation 35 (min-curv) / 38 (min-time: γ² terms),
+    per sample per outer: lin-geom 40, update+normals 14, corridor 2·(Ei+Eo)·8 + (Ei or Eo)·14."""
+    per_eval = 38.0 if mintime else 35.0
+    fl = N * (per_eval * E_k + 40 + 14 + 16 * Eseg + 7 * Eseg)
+    if mintime:
+        fl += N * (30 + 2 * 25 * S + 20)   # κ, v-pass sweeps (fwd+bwd step ≈25 flops), γ²
+    return fl
+
+
+def bytes_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: float = 0.0) -> float:
+    """SURVEY.md §8d streaming model (8-B words, each array once per pass)."""
+    if mintime:
+        return N * (88 * E_k + 224 + 24 + 48 * S + 32) + 32 * Eseg
+    return N * (80 * E_k + 224) + 32 * Eseg
+
+
+def read_pmc_traffic(tag: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), or None."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(tag, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(prob, cfg, budget_s: float = 12.0, max_inst: int = 64):
+    """Single-thread C oracle on a bounded sample of the same workload (seeds 0..)."""
+    import oracle_lib as O
+
+    seeds = np.arange(max_inst, dtype=np.uint64)
+    done = 0
+    t0 = time.perf_counter()
+    while done < max_inst and time.perf_counter() - t0 < budget_s:
+        O.run_oracle(prob, cfg, seeds=seeds, B=max_inst, modes=(True, False), b_range=(done, done + 1))
+        done += 1
+    dt = time.perf_counter() - t0
+    outers = done * int(cfg.max_outer_iters)
+    return {"value": outers / dt, "unit": "PGD outer-iters/s", "cores": 1, "kind": "port",
+            "sample": f"{done} instances (seeds 0..{done - 1}) of C2 min-curv, N={prob.N}, 14 outer each, "
+                      f"{dt:.1f} s, one thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3 min-time lap check")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    lib = abi.load_library()
+    if lib.rl_device_count() < 1:
+        raise SystemExit("bench: no HIP device visible")
+
+    case, prob, cfg = load_problem("cmap1_n2000")
+    B = args.batch
+    N = prob.N
+    MO = int(cfg.max_outer_iters)
+    seeds = np.arange(rank * B, (rank + 1) * B, dtype=np.uint64)     # rank 0 / seed 0 = the reference
+    plan = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=abi.RL_MODE_MINCURV, device=local)
+
+    # results straight into torch tensors (zero-copy for the RCCL gather)
+    f64 = dict(dtype=torch.float64, device=dev)
+    res = {k: torch.empty((B, N), **f64) for k in ("x", "y", "kappa", "alpha_last")}
+    res["evals"] = torch.empty((B, MO), dtype=torch.int32, device=dev)
+    plan.bind_device_outputs(abi.RL_MODE_MINCURV, {k: v.data_ptr() for k, v in res.items()})
+    gathered = None
+    if world > 1 and rank == 0:
+        gathered = {k: [torch.empty_like(v) for _ in range(world)] for k, v in res.items()}
+
+    stream = torch.cuda.Stream(device=dev)
+
+    def step():
+        plan.run(stream.cuda_stream)
+        if world > 1:
+            with torch.cuda.stream(stream):
+                for k, v in res.items():
+                    dist.gather(v, gathered[k] if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        if args.steps <= 50:
+            stream.synchronize()
+            kernel_ms.append(plan.kernel_ms(1))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_outer = world * B * MO * args.steps
+    value = total_outer / elapsed
+    tracks_per_s = world * B * args.steps / elapsed
+
+    if rank != 0:
+        plan.close()
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # ---- parity of this run (outside the timed region) ----
+    evals = res["evals"].cpu().numpy()
+    E_k = float(evals.mean())
+    x0 = res["x"][0].cpu().numpy()
+    al0 = res["alpha_last"][0].cpu().numpy()
+    k0 = res["kappa"][0].cpu().numpy()
+    parity = {
+        "seed0_vs_reference_max_rel_err": float(max(
+            np.max(np.abs(x0 - case["mc_x"])) / np.max(np.abs(case["mc_x"])),
+            np.max(np.abs(al0 - case["mc_alpha_last"])) / np.max(np.abs(case["mc_alpha_last"])),
+            np.max(np.abs(k0 - case["mc_kappa"])) / np.max(np.abs(case["mc_kappa"])))),
+        "tolerance": "1e-4 x column max (+1e-9)",
+    }
+
+    # ---- roofline of the dominant kernel (HIP events on the launch stream) ----
+    Eseg = prob.inner_seg.shape[0] + prob.outer_seg.shape[0]
+    k_ms = float(np.mean(kernel_ms)) if kernel_ms else plan.kernel_ms(1)
+    fl_launch = B * MO * flops_per_outer(N, E_k, Eseg)
+    by_launch = B * MO * bytes_per_outer(N, E_k, Eseg)
+    achieved_tf = fl_launch / (k_ms * 1e-3) / 1e12
+    roofline = {
+        "bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 4), "traffic": read_pmc_traffic("c2_mincurv"),
+        "kernel": "rl_optimize_kernel<8,256,closed,mincurv>", "kernel_ms": round(k_ms, 3),
+        "note": "fp64 compute roof (VALU; MI355X fp64 vector = fp64 dense-matrix peak = 78.6 TF): "
+                "the instance state stays in VGPR/LDS, so HBM is not the binding roof",
+        "streaming_model_GBps": round(by_launch / (k_ms * 1e-3) / 1e9, 1),
+        "streaming_model_frac_of_hbm": round(by_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
+        "evals_per_outer": round(E_k, 2),
+    }
+
+    extras = {}
+    if not args.no_extras:
+        # C3 min-time lap check (N=2000, max_vpass_iters=20): seed 0 vs the reference lap
+        c3, p3, cfg3 = load_problem("cmap1_n2000_vp20")
+        Bm = 256 if world == 1 else 64
+        pl3 = raceline.Plan(p3, cfg3, seeds=np.arange(Bm, dtype=np.uint64), B=Bm,
+                            modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, device=local)
+        pl3.run()
+        mc3, mt3 = pl3.fetch()
+        t1 = time.perf_counter()
+        pl3.run()
+        pl3.fetch()
+        t3 = time.perf_counter() - t1
+        lap_ref = float(c3["mt_lap"])
+        extras["c3_mintime_plus_mincurv"] = {
+            "instances": Bm, "wall_ms": round(t3 * 1e3, 2),
+            "outer_iters_per_s": round(2 * Bm * MO / t3, 1),
+            "kernel_ms_mincurv": round(pl3.kernel_ms(1), 3), "kernel_ms_mintime": round(pl3.kernel_ms(2), 3),
+            "lap_seed0_s": float(mt3.lap[0]), "lap_ref_s": lap_ref,
+            "lap_delta_s": float(abs(mt3.lap[0] - lap_ref)),
+            "lap_mean_over_seeds_s": float(np.mean(mt3.lap)),
+            "vpass_sweeps_mean": float(np.mean(mt3.vpass_sweeps)),
+        }
+        pl3.close()
+
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(prob, cfg)
+
+    out = {
+        "metric": "PGD outer-iters/sec (N=2000 samples, closed, competition_map1, 1024 alpha-seeds/GPU, min-curv)",
+        "value": round(value, 1),
+        "unit": "PGD outer-iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "competition_map1 cones from the reference repo -> reference steps 1-6 (fixture); synthetic alpha-seeds",
+        "config": {"workload": "C2: competition_map1 closed, N=2000, B=1024 alpha-seeds per GPU, min-curvature, "
+                               "14 outer iterations, default cfg::Config", "N": N, "batch_per_gpu": B,
+                   "global_batch": world * B, "parallelism": f"instances sharded over {world} GPU(s), RCCL gather"},
+        "tracks_per_s": round(tracks_per_s, 2),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "parity": parity,
+        **extras,
+    }
+    print(json.dumps(out), flush=True)
+    plan.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -175,6 +175,11 @@ int rl_plan_fetch(rl_plan* plan, rl_out* out_mincurv, rl_out* out_mintime);
 /* which: RL_MODE_MINCURV or RL_MODE_MINTIME; fills device pointers (same layout as
  * rl_out, NULL where the mode does not produce the field). */
 int rl_plan_device_outputs(rl_plan* plan, int32_t which, rl_out* dev_out);
+/* Bind caller-owned DEVICE buffers (same layout as rl_out: [B][N] arrays, lap [B],
+ * evals/accepts [B][max_outer_iters], vpass_sweeps [B][max_outer_iters+1]) as the
+ * result storage of mode `which`; NULL fields keep the plan's own buffers.  Lets a
+ * framework (e.g. torch tensors for an RCCL gather) receive results without copies. */
+int rl_plan_bind_device_outputs(rl_plan* plan, int32_t which, const rl_out* dev_out);
 /* per-kernel device time of the last run, in ms, measured with HIP events on the
  * run stream (index 0 = main optimisation kernel, 1 = prepare, 2 = finalize).  */
 int rl_plan_kernel_ms(rl_plan* plan, int32_t idx, float* ms);

@@ -293,6 +293,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_plan_fetch.restype = C.c_int
     lib.rl_plan_device_outputs.argtypes = [C.c_void_p, C.c_int32, C.POINTER(RlOut)]
     lib.rl_plan_device_outputs.restype = C.c_int
+    lib.rl_plan_bind_device_outputs.argtypes = [C.c_void_p, C.c_int32, C.POINTER(RlOut)]
+    lib.rl_plan_bind_device_outputs.restype = C.c_int
     lib.rl_plan_kernel_ms.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_float)]
     lib.rl_plan_kernel_ms.restype = C.c_int
     lib.rl_plan_destroy.argtypes = [C.c_void_p]

@@ -181,8 +181,8 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
     if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
     if (prob->N < 0) return fail(RL_EINVAL, "N < 0");
     if ((modes & (RL_MODE_MINCURV | RL_MODE_MINTIME)) == 0 || (modes & ~3)) return fail(RL_EINVAL, "bad modes");
-    if (prob->N > 0 && (!prob->center_xy || !(prob->L > 0) || !std::isfinite(prob->L)))
-        return fail(RL_EINVAL, "center_xy NULL or L not positive/finite");
+    // any L is accepted like the reference (h = L/N, ref:690); only the pointer is checked
+    if (prob->N > 0 && !prob->center_xy) return fail(RL_EINVAL, "center_xy is NULL");
     if (prob->Ei < 0 || prob->Eo < 0 || (prob->Ei > 0 && !prob->inner_seg) || (prob->Eo > 0 && !prob->outer_seg))
         return fail(RL_EINVAL, "bad segments");
     const int mo = cfg[0].max_outer_iters;
@@ -347,6 +347,28 @@ int rl_plan_fetch(rl_plan* p, rl_out* out_mc, rl_out* out_mt) {
     int rc;
     if ((rc = fetch_mode(p, 0, out_mc, st)) || (rc = fetch_mode(p, 1, out_mt, st))) return rc;
     HIPCHK(hipStreamSynchronize(st));
+    return RL_OK;
+}
+
+int rl_plan_bind_device_outputs(rl_plan* p, int32_t which, const rl_out* d) {
+    if (!p || !d) return fail(RL_EINVAL, "NULL argument");
+    int m = (which == RL_MODE_MINCURV) ? 0 : (which == RL_MODE_MINTIME ? 1 : -1);
+    if (m < 0 || !(p->modes & which)) return fail(RL_EINVAL, "mode not in plan");
+    ModeBufs& mb = p->mb[m];
+    if (d->x) mb.x = d->x;
+    if (d->y) mb.y = d->y;
+    if (d->heading) mb.heading = d->heading;
+    if (d->kappa) mb.kappa = d->kappa;
+    if (d->alpha_total) mb.alpha_total = d->alpha_total;
+    if (d->alpha_last) mb.alpha_last = d->alpha_last;
+    if (m == 1) {
+        if (d->v) mb.v = d->v;
+        if (d->ax) mb.ax = d->ax;
+        if (d->lap) mb.lap = d->lap;
+        if (d->vpass_sweeps) mb.sweeps = d->vpass_sweeps;
+    }
+    if (d->evals) mb.evals = d->evals;
+    if (d->accepts) mb.accepts = d->accepts;
     return RL_OK;
 }
 

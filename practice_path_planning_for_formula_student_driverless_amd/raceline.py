@@ -155,6 +155,15 @@ class Plan:
         _check(_lib().rl_plan_device_outputs(self._h, which, C.byref(d)))
         return d
 
+    def bind_device_outputs(self, which: int, ptrs: dict) -> None:
+        """Use caller-owned device buffers (name -> device pointer int, e.g. a
+        torch tensor's data_ptr()) as result storage for mode `which`."""
+        d = abi.RlOut()
+        for name, ptr in ptrs.items():
+            typ = C.POINTER(C.c_int32) if name in ("evals", "accepts", "vpass_sweeps") else C.POINTER(C.c_double)
+            setattr(d, name, C.cast(C.c_void_p(ptr), typ))
+        _check(_lib().rl_plan_bind_device_outputs(self._h, which, C.byref(d)))
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             _lib().rl_plan_destroy(self._h)

@@ -32,7 +32,7 @@ def declared_functions():
 def test_header_declares_expected_entry_points():
     names = declared_functions()
     for must in ("rl_optimize", "rl_plan_create", "rl_plan_run", "rl_plan_fetch", "rl_plan_destroy",
-                 "rl_plan_device_outputs", "rl_plan_kernel_ms", "rl_cfg_default", "rl_cfg_set_mu",
+                 "rl_plan_device_outputs", "rl_plan_kernel_ms", "rl_plan_bind_device_outputs", "rl_cfg_default", "rl_cfg_set_mu",
                  "rl_ring_segments", "rl_seed_value", "rl_device_count", "rl_last_error", "rl_abi_version",
                  "rl_kernel_variant"):
         assert must in names

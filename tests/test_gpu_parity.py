@@ -126,6 +126,8 @@ def _synthetic(N, closed, rng):
     inner = np.stack([18.0 * np.cos(k) * 1.5, 18.0 * np.sin(k)], axis=1)
     outer = np.stack([22.0 * np.cos(k) * 1.5, 22.0 * np.sin(k)], axis=1)
     L = float(np.sum(np.hypot(*np.diff(np.vstack([center, center[:1]]), axis=0).T)))
+    if N < 3:
+        L = 2 * np.pi * 20.0   # a one/two-point "track" has no length of its own
     return abi.Problem(center=center, L=L, inner_seg=raceline.edges_for(inner, closed),
                        outer_seg=raceline.edges_for(outer, closed), veh_width=1.0, closed=closed)
 
