@@ -52,6 +52,16 @@ def build_lib(force: bool = False) -> str:
     return out
 
 
+def build_variant(name: str, defines: dict) -> str:
+    """Experiment build: _lib/variants/librl_<name>.so with -D overrides (A/B timing only)."""
+    vdir = os.path.join(LIB_DIR, "variants")
+    os.makedirs(vdir, exist_ok=True)
+    out = os.path.join(vdir, f"librl_{name}.so")
+    flags = [f"-D{k}={v}" for k, v in defines.items()]
+    _run([HIPCC, *HIP_FLAGS, *flags, "-shared", *KERNEL_SRCS, "-o", out], cwd=PKG)
+    return out
+
+
 def build_host(force: bool = False) -> str:
     """host/raceline.cpp -> _lib/fsd_raceline, linked against librl.so (rpath $ORIGIN)."""
     lib = build_lib(force)

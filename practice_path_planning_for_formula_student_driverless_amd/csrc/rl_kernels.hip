@@ -38,10 +38,26 @@ namespace rl {
 constexpr int CK = 4;   // corridor sub-chunk (samples per ray-scan pass)
 
 // ------------------------------------------------------------ wave primitives
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+// wave-uniform sum of x over the 64 lanes: DPP butterflies inside each 16-lane row
+// (quad_perm, row_ror:4, row_ror:8), then the four row sums via readlane, combined
+// in a fixed order.  No LDS round trip.
 __device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
+    x += dpp<0xB1>(x);    // quad_perm [1,0,3,2]
+    x += dpp<0x4E>(x);    // quad_perm [2,3,0,1]
+    x += dpp<0x124>(x);   // row_ror:4
+    x += dpp<0x128>(x);   // row_ror:8
+    return (readlane(x, 0) + readlane(x, 16)) + (readlane(x, 32) + readlane(x, 48));
 }
 // lane l <- lane l-1 (DPP wave_shr:1); lane 0 gets 0
 __device__ __forceinline__ double dpp_from_left(double x) {
@@ -96,18 +112,34 @@ struct alignas(16) Smem {
     double eF[4][NW];            // per exchange slot: lane-0 first value of each wave
     double eL[4][NW];            //                    lane-63 last value of each wave
     double wL[4];                // last valid value of the last active thread (closed wrap)
+    double sink[64];             // target of the lanes that publish nothing (branch-free stores)
     double red[3][NW];           // per-wave partial sums of an evaluation
     double red2[2][NW];          // other block reductions
     double bc[4];                // broadcast scalars
 };
 
 // --------------------------------------------------------------- the kernel
+// Variant for 1024 < N <= 2048 (the C2/C3 tracks): RL_MID_K samples per lane,
+// RL_MID_T lanes per instance, RL_MID_W waves per SIMD requested from the
+// register allocator.  Build-time knobs so variants can be A/B-timed.
+#ifndef RL_MID_K
+#define RL_MID_K 8
+#endif
+#ifndef RL_MID_T
+#define RL_MID_T 256
+#endif
+#ifndef RL_MID_W
+#define RL_MID_W 2
+#endif
+
 // waves per SIMD to keep resident (caps the register budget the compiler may use)
-template <int T>
-struct MinWaves { static constexpr int value = (T >= 512) ? 1 : (T == 64 ? 4 : 2); };
+template <int K, int T>
+struct MinWaves {
+    static constexpr int value = (K == RL_MID_K && T == RL_MID_T) ? RL_MID_W : ((T >= 512) ? 1 : (T == 64 ? 4 : 2));
+};
 
 template <int K, int T, bool CLOSED, bool MT>
-__global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KParams p) {
+__global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel(KParams p) {
     constexpr int NW = T / 64;
     __shared__ Smem<K, T> sm;
 
@@ -118,6 +150,13 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
     const int cnt = min(K, max(0, N - base));
     const int Ta = (N + K - 1) / K;
     const bool active = tid < Ta;
+    const int cntL = N - (Ta - 1) * K;                  // samples of the last active thread
+    // wave-uniform: does this wave hold the (only) partial chunk?  Every other
+    // lane is either full (cnt == K) or inactive, and inactive lanes carry exact
+    // zeros (coefficients, corridor, state, neighbour values), so their sums
+    // need no masking.
+    const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+    const bool part_wave = (cntL != K) && (((Ta - 1) >> 6) == wid_u);
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
@@ -142,22 +181,29 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
         const double first = a[0], last = a[K - 1];
         dl = dpp_from_left(last);
         dr = dpp_from_right(first);
-        if (lane == 0) sm.eF[slot][wid] = first;
-        if (lane == 63) sm.eL[slot][wid] = last;
-        if (tid == Ta - 1) sm.wL[slot] = (cnt == K) ? last : pick(a, cnt - 1);
+        *((lane == 0) ? &sm.eF[slot][wid] : &sm.sink[lane]) = first;
+        *((lane == 63) ? &sm.eL[slot][wid] : &sm.sink[lane]) = last;
+        if (cntL == K) {
+            *((tid == Ta - 1) ? &sm.wL[slot] : &sm.sink[lane]) = last;
+        } else if (part_wave) {
+            const double lv = pick(a, cntL - 1);
+            if (tid == Ta - 1) sm.wL[slot] = lv;
+        }
     };
     // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped)
     auto xget = [&](int slot, double dl, double dr, double& lv, double& rv) RL_AI {
-        lv = dl;
-        if (lane == 0) lv = (wid > 0) ? sm.eL[slot][wid - 1] : sm.wL[slot];
-        rv = dr;
-        if (lane == 63 && wid + 1 < NW) rv = sm.eF[slot][wid + 1];
-        if (tid == Ta - 1) rv = sm.eF[slot][0];
+        const double el = (wid > 0) ? sm.eL[slot][(wid > 0) ? wid - 1 : 0] : sm.wL[slot];   // wave-uniform reads
+        const double ef = sm.eF[slot][(wid + 1 < NW) ? wid + 1 : 0];
+        const double e0 = sm.eF[slot][0];
+        lv = (lane == 0) ? el : dl;
+        rv = (lane == 63) ? ef : dr;
+        if (tid == Ta - 1) rv = e0;
+        if (!active) { lv = 0.0; rv = 0.0; }
     };
     // the last active thread's padding slots take the right neighbour, so every
     // stencil reads a[k+1] (k<K-1) or rv (k=K-1) uniformly
     auto fill_pad = [&](double (&a)[K], double rv) RL_AI {
-        if (cnt != K) {
+        if (part_wave && cnt != K && active) {
 #pragma unroll
             for (int k = 0; k < K; ++k) a[k] = (k < cnt) ? a[k] : rv;
         }
@@ -250,15 +296,22 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
 #pragma unroll
                     for (int k = 0; k < CK; ++k) {
                         double den = ux[k] * (-s.vy) + uy[k] * (s.vx);
-                        if (fabs(den) < 1e-15) continue;
                         double ax = s.x0 - qx[k], ay = s.y0 - qy[k];
-                        double inv = 1.0 / den;
-                        double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
-                        double u = (ux[k] * ay - uy[k] * ax) * inv;
-                        if (u >= -1e-12 && u <= 1.0 + 1e-12) {
-                            if (t > 0.0 && t < bp[k]) bp[k] = t;
-                            double tn = -t;
-                            if (tn > 0.0 && tn < bn[k]) bn[k] = tn;
+                        double nu = ux[k] * ay - uy[k] * ax;          // u = nu * (1/den)
+                        // conservative exact pretest: skip the division unless u can
+                        // land in [-1e-12, 1+1e-12] (u carries <= 2 roundings)
+                        const double ad = fabs(den), anu = fabs(nu);
+                        const bool same = (nu < 0) == (den < 0);
+                        const bool cand = !(ad < 1e-15) && (anu <= 1.0000001 * ad) && (same || anu <= 4e-12 * ad);
+                        if (cand) {
+                            double inv = 1.0 / den;
+                            double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
+                            double u = nu * inv;
+                            if (u >= -1e-12 && u <= 1.0 + 1e-12) {
+                                if (t > 0.0 && t < bp[k]) bp[k] = t;
+                                double tn = -t;
+                                if (tn > 0.0 && tn < bn[k]) bn[k] = tn;
+                            }
                         }
                     }
                 }
@@ -266,15 +319,36 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
             scan(0, Ei, bpi, bni);
             scan(Ei, Ee, bpo, bno);
             // minDistanceToSegments_global fallback (ref:501-512) where a ray missed
+            // Two passes: an upper bound ub >= min distance from the segment start
+            // points, then the exact reference expression only for segments whose
+            // lower bound |P-mid| - half_length does not exceed ub.
             auto mindist = [&](int e0, int e1, double (&md)[CK]) RL_AI {
+                double ub2[CK];
+#pragma unroll
+                for (int k = 0; k < CK; ++k) ub2[k] = INFINITY;
                 for (int e = e0; e < e1; ++e) {
                     const SegRec s = S[e];
 #pragma unroll
                     for (int k = 0; k < CK; ++k) {
-                        double apx = qx[k] - s.x0, apy = qy[k] - s.y0;
-                        double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
-                        double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
-                        md[k] = smin(md[k], hypot_ref(qx[k] - Qx, qy[k] - Qy));
+                        double dx = qx[k] - s.x0, dy = qy[k] - s.y0;
+                        ub2[k] = fmin(ub2[k], dx * dx + dy * dy);
+                    }
+                }
+                double lim[CK];
+#pragma unroll
+                for (int k = 0; k < CK; ++k) lim[k] = sqrt(ub2[k]) * (1.0 + 1e-9) + 1e-12;
+                for (int e = e0; e < e1; ++e) {
+                    const SegRec s = S[e];
+#pragma unroll
+                    for (int k = 0; k < CK; ++k) {
+                        double mx = qx[k] - s.mx, my = qy[k] - s.my;
+                        double r = lim[k] + s.hr;
+                        if (!(mx * mx + my * my > r * r)) {
+                            double apx = qx[k] - s.x0, apy = qy[k] - s.y0;
+                            double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
+                            double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
+                            md[k] = smin(md[k], hypot_ref(qx[k] - Qx, qy[k] - Qy));
+                        }
                     }
                 }
             };
@@ -473,9 +547,14 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
     auto eval_j = [&](double (&a)[K], bool trial, double& dec) RL_AI -> double {
         double pdec = 0.0;
         if (trial) {
+            if (part_wave) {
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (k < cnt) pdec += gr[k] * (a[k] - al[k]);
+                for (int k = 0; k < K; ++k)
+                    if (k < cnt) pdec += gr[k] * (a[k] - al[k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) pdec += gr[k] * (a[k] - al[k]);
+            }
         }
         double dl0, dr0;
         xpub(0, a, dl0, dr0);
@@ -498,7 +577,7 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
             q1[k] = c01.x * Wz;
             q2[k] = c01.y * Wz;
             a1v[k] = x1;
-            if (k < cnt) { pJ += jz; pJsm += x1 * x1; }
+            if (!part_wave || k < cnt) { pJ += jz; pJsm += x1 * x1; }
         }
         xpub(1, q1, dl1, dr1);
         xpub(2, q2, dl2, dr2);
@@ -715,7 +794,9 @@ __global__ __launch_bounds__(T, MinWaves<T>::value) void rl_optimize_kernel(KPar
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     double ai = al[k] - step * gr[k];
-                    an[k] = smin(hi[k], smax(lo[k], ai));
+                    // min(hi, max(lo, ai)) (ref:731) with v_min/v_max_f64: same value
+                    // as the std:: forms incl. NaN handling (only the sign of a zero may differ)
+                    an[k] = fmin(hi[k], fmax(lo[k], ai));
                 }
                 double Jn = eval_j(an, true, dec);
                 ++evals;
@@ -755,27 +836,26 @@ static hipError_t launch_kt(const KParams& p, bool mt, hipStream_t st) {
     return mt ? launch_t<K, T, false, true>(p, st) : launch_t<K, T, false, false>(p, st);
 }
 
-// variant table: (K, T) by N.  K samples per lane, T lanes per instance.
+// variant table by N: (K samples per lane, T lanes per instance)
+//   N <= 256          (4, 64)      one wave per instance
+//   N <= 1024         (8, 128)
+//   N <= 2048         (RL_MID_K, RL_MID_T)   default (8, 256)
+//   N <= 4096         (8, 512)
+static_assert(RL_MID_K * RL_MID_T == 2048, "mid variant must cover N <= 2048");
 int pick_k(int N) {
     if (N <= 4 * 64) return 4;
+    if (N <= 8 * 128) return 8;
+    if (N <= 2048) return RL_MID_K;
     if (N <= 8 * 512) return 8;
     return -1;
-}
-static int pick_t(int N) {
-    if (N <= 4 * 64) return 64;
-    if (N <= 8 * 128) return 128;
-    if (N <= 8 * 256) return 256;
-    return 512;
 }
 
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
-    switch (pick_t(p.N)) {
-        case 64: return launch_kt<4, 64>(p, mintime, st);
-        case 128: return launch_kt<8, 128>(p, mintime, st);
-        case 256: return launch_kt<8, 256>(p, mintime, st);
-        default: return launch_kt<8, 512>(p, mintime, st);
-    }
+    if (p.N <= 4 * 64) return launch_kt<4, 64>(p, mintime, st);
+    if (p.N <= 8 * 128) return launch_kt<8, 128>(p, mintime, st);
+    if (p.N <= 2048) return launch_kt<RL_MID_K, RL_MID_T>(p, mintime, st);
+    return launch_kt<8, 512>(p, mintime, st);
 }
 
 }  // namespace rl

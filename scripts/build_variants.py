@@ -1,0 +1,17 @@
+"""Build A/B variant libraries into _lib/variants/ (experiments only)."""
+import os, sys
+from concurrent.futures import ThreadPoolExecutor
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from practice_path_planning_for_formula_student_driverless_amd import build as B
+VARIANTS = {
+    "base": {},
+    "k4t512w2": {"RL_MID_K": 4, "RL_MID_T": 512, "RL_MID_W": 2},
+    "k4t512w4": {"RL_MID_K": 4, "RL_MID_T": 512, "RL_MID_W": 4},
+}
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    import shutil; shutil.rmtree(os.path.join(B.LIB_DIR, "variants"), ignore_errors=True)
+    with ThreadPoolExecutor(4) as ex:
+        for p in ex.map(lambda n: B.build_variant(n, VARIANTS[n]), names):
+            print("built", p)
