@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -51,7 +52,15 @@ struct ModeBufs {
     double *x = nullptr, *y = nullptr, *heading = nullptr, *kappa = nullptr, *alpha_total = nullptr,
            *alpha_last = nullptr, *v = nullptr, *ax = nullptr, *lap = nullptr, *nx = nullptr, *ny = nullptr;
     int32_t *evals = nullptr, *accepts = nullptr, *sweeps = nullptr;
+    rl::StreamBufs sb{};      // large-N variant only
 };
+
+// variant: register-resident (N <= 4096) unless N is larger or RL_FORCE_STREAM=1 (testing)
+bool use_stream(int N) {
+    if (N > rl::RL_REG_MAX_N) return true;
+    const char* f = std::getenv("RL_FORCE_STREAM");
+    return f && f[0] == '1';
+}
 
 }  // namespace
 
@@ -91,7 +100,11 @@ int rl_device_count(void) {
     return n;
 }
 
+// samples per lane of the register-resident kernel (4 or 8), 1 for the streaming
+// kernel, RL_ETOOBIG beyond it
 int rl_kernel_variant(int32_t N) {
+    if (N > rl::RL_STREAM_MAX_N) return RL_ETOOBIG;
+    if (use_stream(N)) return 1;
     int k = rl::pick_k(N);
     return k < 0 ? RL_ETOOBIG : k;
 }
@@ -191,8 +204,7 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
         if (cfg[c].max_outer_iters < 0 || cfg[c].max_inner_iters < 0 || cfg[c].max_vpass_iters < 0)
             return fail(RL_EINVAL, "negative iteration count");
     }
-    if (prob->N > 0 && rl::pick_k(prob->N) < 0)
-        return fail(RL_ETOOBIG, "N exceeds the register-resident kernel (N <= 4096)");
+    if (prob->N > rl::RL_STREAM_MAX_N) return fail(RL_ETOOBIG, "N exceeds the streaming kernel (N <= 1048576)");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
     if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
@@ -252,6 +264,13 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
                 (rc = p->alloc(&mb.sweeps, (size_t)B * (mo + 1))))
                 return cleanup(rc);
         }
+        if (use_stream(p->N)) {
+            double** arrs[rl::RL_STREAM_ARRAYS] = {&mb.sb.al, &mb.sb.an, &mb.sb.gr, &mb.sb.lo, &mb.sb.hi,
+                                                  &mb.sb.a1, &mb.sb.a2, &mb.sb.n0, &mb.sb.w, &mb.sb.q1,
+                                                  &mb.sb.q2, &mb.sb.d1, &mb.sb.g2, &mb.sb.v, &mb.sb.vs};
+            for (auto a : arrs)
+                if ((rc = p->alloc(a, BN))) return cleanup(rc);
+        }
     }
     if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(RL_EHIP, "upload sync"));
     *out = p;
@@ -291,7 +310,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
         kp.L = p->L; kp.veh_width = p->veh_width;
         HIPCHK(hipEventRecord(p->ev[1 + m], st));
-        hipError_t e = rl::launch_optimize(kp, m == 1, st);
+        hipError_t e = use_stream(p->N) ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
     }
     HIPCHK(hipEventRecord(p->ev[3], st));

@@ -24,9 +24,19 @@ struct KParams {
     double L, veh_width;
 };
 
+// Per-instance HBM state of the large-N streaming kernel (rl_stream.hip), [B][N] each.
+struct StreamBufs {
+    double *al, *an, *gr, *lo, *hi, *a1, *a2, *n0, *w, *q1, *q2, *d1, *g2, *v, *vs;
+};
+constexpr int RL_STREAM_ARRAYS = 15;
+constexpr int RL_REG_MAX_N = 4096;          // register-resident kernel covers N <= 4096
+constexpr int RL_STREAM_MAX_N = 1 << 20;
+
 // samples per lane for N (4 or 8), or -1 if N exceeds the register-resident kernel
 int pick_k(int N);
 // enqueue one persistent launch (one workgroup per instance) on `st`
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
+// large-N variant: one 1024-thread workgroup per instance, state in HBM
+hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st);
 
 }  // namespace rl

@@ -1,0 +1,515 @@
+// rl_stream.hip — large-N (N > 4096) variant of the raceline optimiser for gfx950.
+//
+// Same algorithm and arithmetic as rl_kernels.hip (ref = /root/reference/src/main.cpp:
+// compute_min_curvature_raceline ref:683-764, compute_min_time_raceline ref:905-1052),
+// but the per-instance state no longer fits on chip (N=10000: ~1 MB per instance), so
+// it streams through HBM / L2:
+//   * one 1024-thread workgroup per instance; every state array (α, grad, α_trial,
+//     lo, hi, A1, A2, N0, W, q1, q2, D1α, γ², v, κ) is an instance-major [B][N]
+//     slice in HBM;
+//   * stencil / PGD / corridor / geometry phases use the interleaved mapping
+//     i = tile*1024 + tid: consecutive lanes touch consecutive doubles (coalesced),
+//     neighbour reads i±1 hit the lines the wave just loaded;
+//   * __syncthreads() orders the global writes of one phase before the next phase's
+//     neighbour reads (all waves of the instance share one CU);
+//   * the v(s) relaxation gives each thread a contiguous range [t*C, t*C+C) and
+//     publishes the chunk's outgoing value through LDS, exactly like the
+//     register-resident kernel;
+//   * reductions: per-thread partial sums in a fixed sample order, DPP wave sums,
+//     then the 16 wave partials in order.
+// This is the HBM-bound configuration; its roofline is HBM bytes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_abi.h"
+#include "rl_device.h"
+#include "rl_kernels.h"
+#include "rl_math.h"
+
+namespace rl {
+
+namespace {
+constexpr int TS = 1024;          // threads per instance
+constexpr int NWS = TS / 64;
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_s(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_s(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+__device__ __forceinline__ double wave_sum_s(double x) {
+    x += dpp_s<0xB1>(x);
+    x += dpp_s<0x4E>(x);
+    x += dpp_s<0x124>(x);
+    x += dpp_s<0x128>(x);
+    return (readlane_s(x, 0) + readlane_s(x, 16)) + (readlane_s(x, 32) + readlane_s(x, 48));
+}
+
+struct SSmem {
+    double red[4][NWS];
+    double vin[2][TS];
+    double bc[4];
+};
+
+// block sum of NV values; ends with every thread holding the totals
+template <int NV>
+__device__ __forceinline__ void block_sum_s(SSmem& sm, double (&v)[NV], int lane, int wid) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = wave_sum_s(v[j]);
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) sm.red[j][wid] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        double s = sm.red[j][0];
+        for (int w = 1; w < NWS; ++w) s += sm.red[j][w];
+        v[j] = s;
+    }
+    __syncthreads();
+}
+}  // namespace
+
+template <bool CLOSED, bool MT>
+__global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs sb) {
+    __shared__ SSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int b = blockIdx.x;
+    const int N = p.N;
+    const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
+    const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
+
+    const double h = p.L / (double)N;                    // ref:690 / 913
+    const double invh = 1.0 / h, inv2h = 1.0 / (2 * h), invh2 = 1.0 / (h * h);   // ref:547, 562
+    const double m2invh2 = -2 * invh2;
+    const double two_h = 2 * h, hh = h * h;
+    const double lam = C.lambda_smooth, lam2 = 2.0 * lam;
+
+    const size_t off = (size_t)b * (size_t)N;
+    double* __restrict__ X = p.x + off;
+    double* __restrict__ Y = p.y + off;
+    double* __restrict__ NX = p.nx + off;
+    double* __restrict__ NY = p.ny + off;
+    double* __restrict__ ATOT = p.alpha_total + off;
+    double* __restrict__ ALAST = p.alpha_last + off;
+    double* __restrict__ AL = sb.al + off;
+    double* __restrict__ AN = sb.an + off;               // α and α_trial swap roles on accept
+    double* __restrict__ GR = sb.gr + off;
+    double* __restrict__ LO = sb.lo + off;
+    double* __restrict__ HI = sb.hi + off;
+    double* __restrict__ CA1 = sb.a1 + off;
+    double* __restrict__ CA2 = sb.a2 + off;
+    double* __restrict__ CN0 = sb.n0 + off;
+    double* __restrict__ CW = sb.w + off;
+    double* __restrict__ Q1 = sb.q1 + off;
+    double* __restrict__ Q2 = sb.q2 + off;
+    double* __restrict__ D1 = sb.d1 + off;
+    double* __restrict__ G2 = sb.g2 + off;
+    double* __restrict__ KA = p.kappa + off;          // κ scratch, final output at the end
+    double* __restrict__ V = sb.v + off;
+    double* __restrict__ VS = sb.vs + off;
+
+    auto wrap = [&](int g) -> int {
+        if (CLOSED) { g %= N; if (g < 0) g += N; return g; }
+        return g < 0 ? 0 : (g >= N ? N - 1 : g);
+    };
+    // deriv lambdas of ref:599-613 / 625-639 at sample i
+    auto deriv = [&](int i, double& xp, double& yp, double& xpp, double& ypp) {
+        if (N == 1) { xp = 1; yp = 0; xpp = ypp = 0; return; }
+        if (CLOSED) {
+            const int ip = wrap(i + 1), im = wrap(i - 1);
+            xp = (X[ip] - X[im]) / two_h; yp = (Y[ip] - Y[im]) / two_h;
+            xpp = (X[ip] - 2 * X[i] + X[im]) / hh; ypp = (Y[ip] - 2 * Y[i] + Y[im]) / hh;
+        } else if (i == 0) {
+            xp = (X[1] - X[0]) / h; yp = (Y[1] - Y[0]) / h;
+            if (N >= 3) { xpp = (X[2] - 2 * X[1] + X[0]) / hh; ypp = (Y[2] - 2 * Y[1] + Y[0]) / hh; }
+            else xpp = ypp = 0;
+        } else if (i == N - 1) {
+            xp = (X[N - 1] - X[N - 2]) / h; yp = (Y[N - 1] - Y[N - 2]) / h;
+            if (N >= 3) { xpp = (X[N - 1] - 2 * X[N - 2] + X[N - 3]) / hh; ypp = (Y[N - 1] - 2 * Y[N - 2] + Y[N - 3]) / hh; }
+            else xpp = ypp = 0;
+        } else {
+            xp = (X[i + 1] - X[i - 1]) / two_h; yp = (Y[i + 1] - Y[i - 1]) / two_h;
+            xpp = (X[i + 1] - 2 * X[i] + X[i - 1]) / hh; ypp = (Y[i + 1] - 2 * Y[i] + Y[i - 1]) / hh;
+        }
+    };
+    // normals_from_points_generic ref:581-593
+    auto normal_at = [&](int i) {
+        double tx, ty;
+        if (N == 1) { tx = 1; ty = 0; }
+        else if (CLOSED) { const int ip = wrap(i + 1), im = wrap(i - 1); tx = (X[ip] - X[im]) * 0.5; ty = (Y[ip] - Y[im]) * 0.5; }
+        else if (i == 0) { tx = X[1] - X[0]; ty = Y[1] - Y[0]; }
+        else if (i == N - 1) { tx = X[N - 1] - X[N - 2]; ty = Y[N - 1] - Y[N - 2]; }
+        else { tx = (X[i + 1] - X[i - 1]) * 0.5; ty = (Y[i + 1] - Y[i - 1]) * 0.5; }
+        if (sqrt(tx * tx + ty * ty) < 1e-15) { tx = 1; ty = 0; }
+        double vx = -ty, vy = tx;
+        double n = sqrt(vx * vx + vy * vy);
+        double ox = 0, oy = 0;
+        if (!(n < 1e-15)) { ox = vx / n; oy = vy / n; }
+        NX[i] = ox;
+        NY[i] = oy;
+    };
+    // corridor (ref:694-711 / 749-756) at sample i, both ray directions per segment
+    const SegRec* __restrict__ S = p.seg;
+    auto corridor_at = [&](int i, double guard) {
+        const double qx = X[i], qy = Y[i], ux = NX[i], uy = NY[i];
+        double bp[2] = {INFINITY, INFINITY}, bn[2] = {INFINITY, INFINITY}, md[2] = {INFINITY, INFINITY};
+        const int e_lo[2] = {0, p.Ei}, e_hi[2] = {p.Ei, p.Ei + p.Eo};
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            for (int e = e_lo[r]; e < e_hi[r]; ++e) {
+                const SegRec s = S[e];
+                double den = ux * (-s.vy) + uy * (s.vx);
+                double ax = s.x0 - qx, ay = s.y0 - qy;
+                double nu = ux * ay - uy * ax;
+                const double ad = fabs(den), anu = fabs(nu);
+                const bool same = (nu < 0) == (den < 0);
+                if (!(ad < 1e-15) && (anu <= 1.0000001 * ad) && (same || anu <= 4e-12 * ad)) {
+                    double inv = 1.0 / den;
+                    double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
+                    double u = nu * inv;
+                    if (u >= -1e-12 && u <= 1.0 + 1e-12) {
+                        if (t > 0.0 && t < bp[r]) bp[r] = t;
+                        double tn = -t;
+                        if (tn > 0.0 && tn < bn[r]) bn[r] = tn;
+                    }
+                }
+            }
+            if (!isfinite(bp[r]) || !isfinite(bn[r])) {   // minDistanceToSegments_global ref:501-512
+                double ub2 = INFINITY;
+                for (int e = e_lo[r]; e < e_hi[r]; ++e) {
+                    double dx = qx - S[e].x0, dy = qy - S[e].y0;
+                    ub2 = fmin(ub2, dx * dx + dy * dy);
+                }
+                const double lim = sqrt(ub2) * (1.0 + 1e-9) + 1e-12;
+                for (int e = e_lo[r]; e < e_hi[r]; ++e) {
+                    const SegRec s = S[e];
+                    double mx = qx - s.mx, my = qy - s.my, rr = lim + s.hr;
+                    if (!(mx * mx + my * my > rr * rr)) {
+                        double apx = qx - s.x0, apy = qy - s.y0;
+                        double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
+                        double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
+                        md[r] = smin(md[r], hypot_ref(qx - Qx, qy - Qy));
+                    }
+                }
+            }
+        }
+        auto safe = [](double t, double m) {
+            if (!isfinite(t)) t = m;
+            if (!isfinite(t)) t = 0.0;
+            return smax(0.0, t);
+        };
+        double dpos = smin(safe(bp[0], md[0]), safe(bp[1], md[1]));
+        double dneg = smin(safe(bn[0], md[0]), safe(bn[1], md[1]));
+        double hk = smax(0.0, dpos - guard);
+        double lk = -smax(0.0, dneg - guard);
+        if (!isfinite(hk)) hk = 0.0;
+        if (!isfinite(lk)) lk = 0.0;
+        HI[i] = hk;
+        LO[i] = lk;
+    };
+    // difference operators at sample i (DiffOps / DiffOpsOpen ref:545-579)
+    auto d1_at = [&](int i, double am, double a0, double ap) -> double {
+        if (CLOSED) return (ap - am) * inv2h;
+        if (N == 1) return 0.0;
+        if (i == 0) return (ap - a0) * invh;
+        if (i == N - 1) return (a0 - am) * invh;
+        return (ap - am) * inv2h;
+    };
+    auto d2_at = [&](int i, double am, double a0, double ap) -> double {
+        if (CLOSED) return (ap - 2 * a0 + am) * invh2;
+        if (N <= 2 || i == 0 || i == N - 1) return 0.0;
+        return (ap - 2 * a0 + am) * invh2;
+    };
+    auto d1t_at = [&](int j, double vm, double v0, double vp) -> double {
+        if (CLOSED) return (vm - vp) * inv2h;
+        if (N <= 1) return 0.0;
+        double acc = 0.0;
+        if (j >= 1) acc += ((j == 1) ? invh : inv2h) * vm;
+        if (j == 0) acc += (-invh) * v0;
+        else if (j == N - 1) acc += (+invh) * v0;
+        if (j <= N - 2) acc += ((j + 1 == N - 1) ? -invh : -inv2h) * vp;
+        return acc;
+    };
+    auto d2t_at = [&](int j, double vm, double v0, double vp) -> double {
+        if (CLOSED) return (vp - 2 * v0 + vm) * invh2;
+        if (N <= 2) return 0.0;
+        double acc = 0.0;
+        if (j - 1 >= 1 && j - 1 <= N - 2) acc += (+invh2) * vm;
+        if (j >= 1 && j <= N - 2) acc += m2invh2 * v0;
+        if (j + 1 >= 1 && j + 1 <= N - 2) acc += (+invh2) * vp;
+        return acc;
+    };
+
+    // ---- v(s) profile (ref:782-862), contiguous ranges [t*Cr, t*Cr+Cr) --------
+    VConst vc;
+    vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;
+    vc.a_total2 = vc.a_total * vc.a_total;
+    vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;
+    vc.Fr = C.mass_kg * 9.81 * C.c_rr;
+    vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
+    vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
+    vc.h = h; vc.two_h = 2.0 * h;
+    const int Cr = (N + TS - 1) / TS;
+    const int r0 = min(N, tid * Cr), r1 = min(N, r0 + Cr);
+    const bool ract = r0 < r1;
+    const bool has_left = ract && r0 > 0, has_right = ract && r1 < N;
+    auto vpass = [&]() -> int {
+        for (int i = r0; i < r1; ++i) {
+            double kk = fabs(KA[i]);
+            V[i] = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
+        }
+        int sweeps = 0;
+        for (int s = 0; s < C.max_vpass_iters; ++s) {
+            ++sweeps;
+            for (int i = r0; i < r1; ++i) VS[i] = V[i];           // sweep start
+            __syncthreads();
+            // forward (ref:829-833)
+            double in_prev = -1.0;
+            for (int it = 0;; ++it) {
+                double in = INFINITY;
+                if (it > 0 && has_left) in = sm.vin[(it - 1) & 1][tid - 1];
+                bool changed = false;
+                if (ract && in != in_prev) {
+                    changed = (it > 0);
+                    in_prev = in;
+                    double cur = has_left ? smin(VS[r0], in) : VS[r0];
+                    V[r0] = cur;
+                    for (int i = r0; i + 1 < r1; ++i) {
+                        cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
+                        V[i + 1] = cur;
+                    }
+                    if (has_right) sm.vin[it & 1][tid] = vstep_fwd(vc, cur, KA[r1 - 1]);
+                } else if (has_right) {
+                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
+                }
+                if (!__syncthreads_or(changed) && it > 0) break;
+            }
+            if (CLOSED) {                                          // ref:834-839
+                if (ract && r1 == N) sm.bc[0] = vstep_fwd(vc, V[N - 1], KA[N - 1]);
+                __syncthreads();
+                if (tid == 0) V[0] = smin(V[0], sm.bc[0]);
+                __syncthreads();
+            }
+            // backward (ref:841-845)
+            for (int i = r0; i < r1; ++i) Q1[i] = V[i];            // pass start (Q1 is free here)
+            __syncthreads();
+            in_prev = -1.0;
+            for (int it = 0;; ++it) {
+                double in = INFINITY;
+                if (it > 0 && has_right) in = sm.vin[(it - 1) & 1][tid + 1];
+                bool changed = false;
+                if (ract && in != in_prev) {
+                    changed = (it > 0);
+                    in_prev = in;
+                    double cur = has_right ? smin(Q1[r1 - 1], in) : Q1[r1 - 1];
+                    V[r1 - 1] = cur;
+                    for (int i = r1 - 2; i >= r0; --i) {
+                        cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
+                        V[i] = cur;
+                    }
+                    if (has_left) sm.vin[it & 1][tid] = vstep_bwd(vc, cur, KA[r0]);
+                } else if (has_left) {
+                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
+                }
+                if (!__syncthreads_or(changed) && it > 0) break;
+            }
+            if (CLOSED) {                                          // ref:846-850
+                if (tid == 0) sm.bc[1] = vstep_bwd(vc, V[0], KA[0]);
+                __syncthreads();
+                if (ract && r1 == N) V[N - 1] = smin(V[N - 1], sm.bc[1]);
+                __syncthreads();
+            }
+            bool any = false;
+            for (int i = r0; i < r1; ++i) any |= (V[i] != VS[i]);
+            if (!__syncthreads_or(any)) break;
+        }
+        return sweeps;
+    };
+
+    // ---- init ---------------------------------------------------------------
+    for (int i = tid; i < N; i += TS) {
+        X[i] = p.center[2 * i];
+        Y[i] = p.center[2 * i + 1];
+        ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0; GR[i] = 0.0;
+    }
+    const int MO = C.max_outer_iters;
+    double* al_p = AL;
+    double* an_p = AN;
+    for (int outer = 0;; ++outer) {
+        __syncthreads();
+        if (outer > 0) {                                           // ref:743-746
+            for (int i = tid; i < N; i += TS) {
+                const double a = al_p[i];
+                ALAST[i] = a;
+                X[i] += NX[i] * a;
+                Y[i] += NY[i] * a;
+                ATOT[i] += a;
+                al_p[i] = 0.0;                                     // ref:757
+                GR[i] = 0.0;
+            }
+            __syncthreads();
+        }
+        if (outer < MO) {
+            for (int i = tid; i < N; i += TS) normal_at(i);
+            __syncthreads();
+            const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
+            for (int i = tid; i < N; i += TS) {
+                corridor_at(i, guard);
+                if (outer == 0 && seed != 0)
+                    al_p[i] = smin(HI[i], smax(LO[i], seed_value(seed, i, RL_SEED_SIGMA)));
+            }
+        }
+        if (MT || outer == MO) {
+            for (int i = tid; i < N; i += TS) {                    // ref:595-620
+                double xp, yp, xpp, ypp;
+                deriv(i, xp, yp, xpp, ypp);
+                KA[i] = (xp * ypp - yp * xpp) / pow15(smax(1e-12, xp * xp + yp * yp));
+                if (outer == MO) p.heading[off + i] = atan2(yp, xp);
+            }
+            __syncthreads();
+        }
+        if (MT) {
+            const int sw = vpass();                                // ref:947 / 1047
+            if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
+            __syncthreads();
+            if (outer == MO) {
+                double lt[1] = {0.0};
+                for (int i = tid; i < N; i += TS) {                // ref:854-860
+                    const int j = (i + 1 < N) ? i + 1 : (CLOSED ? 0 : i);
+                    const double v0 = V[i], v1 = V[j];
+                    p.ax[off + i] = (v1 * v1 - v0 * v0) / (2.0 * h);
+                    p.v[off + i] = v0;
+                    lt[0] += h / smax(1e-6, v0);
+                }
+                block_sum_s<1>(sm, lt, lane, wid);
+                if (tid == 0 && p.lap) p.lap[b] = lt[0];
+            } else {
+                double v_avg = 0.0;
+                if (C.time_weight_use_inv_v) {
+                    double vs[1] = {0.0};
+                    for (int i = tid; i < N; i += TS) vs[0] += V[i];
+                    block_sum_s<1>(sm, vs, lane, wid);
+                    v_avg = vs[0] / (double)(N > 1 ? N : 1);
+                }
+                for (int i = tid; i < N; i += TS) {                // ref:950-977
+                    double vkappa = sqrt(C.a_lat_max / smax(fabs(KA[i]), C.kappa_eps));
+                    double rr = smin(1.0, V[i] / smax(1e-6, vkappa));
+                    double r = smin(1.0, smax(0.0, rr * rr));
+                    double rp = (C.time_gamma_power == 2.0) ? r * r : pow(r, C.time_gamma_power);
+                    double corner_w = 1.0 + C.w_time_gain * rp;
+                    double invv_w = 1.0;
+                    if (C.time_weight_use_inv_v) {
+                        double ratio = v_avg / smax(1e-6, V[i]);
+                        invv_w = 1.0 + C.inv_v_gain * (ratio - 1.0);
+                        if (invv_w < 1.0) invv_w = 1.0;
+                        if (invv_w > 3.0) invv_w = 3.0;
+                    }
+                    double gamma = corner_w * invv_w;
+                    G2[i] = gamma * gamma;
+                }
+            }
+        }
+        if (outer == MO) break;
+
+        for (int i = tid; i < N; i += TS) {                        // ref:622-651
+            double xp, yp, xpp, ypp;
+            deriv(i, xp, yp, xpp, ypp);
+            const double nx = NX[i], ny = NY[i];
+            CA1[i] = nx * ypp - ny * xpp;
+            CA2[i] = xp * ny - yp * nx;
+            CN0[i] = xp * ypp - yp * xpp;
+            CW[i] = 1.0 / pow15(smax(1e-12, xp * xp + yp * yp));
+        }
+        __syncthreads();
+
+        // one evaluation of the vector `a` (already written and synchronised):
+        // J and the Armijo decrease; q1,q2,D1α to global for the gradient
+        auto eval_j = [&](const double* a, bool trial, double& dec) -> double {
+            double s3[3] = {0.0, 0.0, 0.0};
+            for (int i = tid; i < N; i += TS) {
+                const double am = a[wrap(i - 1)], a0 = a[i], ap = a[wrap(i + 1)];
+                const double x1 = d1_at(i, am, a0, ap), x2 = d2_at(i, am, a0, ap);
+                const double w = CW[i], A1 = CA1[i], A2 = CA2[i];
+                const double r = w * (CN0[i] + A1 * x1 + A2 * x2);
+                double jz, Wz;
+                if (MT) { const double g2 = G2[i]; jz = g2 * r * r; Wz = w * g2 * r; }
+                else { jz = r * r; Wz = w * r; }
+                Q1[i] = A1 * Wz;
+                Q2[i] = A2 * Wz;
+                D1[i] = x1;
+                s3[0] += jz;
+                s3[1] += x1 * x1;
+                if (trial) s3[2] += GR[i] * (a0 - al_p[i]);
+            }
+            block_sum_s<3>(sm, s3, lane, wid);                     // two barriers: q/D1 visible after
+            dec = s3[2];
+            return s3[0] + lam * s3[1];
+        };
+        auto eval_grad = [&]() {
+            for (int i = tid; i < N; i += TS) {
+                const int im = wrap(i - 1), ip = wrap(i + 1);
+                const double g1 = d1t_at(i, Q1[im], Q1[i], Q1[ip]);
+                const double g2 = d2t_at(i, Q2[im], Q2[i], Q2[ip]);
+                const double gsm = d1t_at(i, D1[im], D1[i], D1[ip]);
+                GR[i] = 2.0 * (g1 + g2) + lam2 * gsm;
+            }
+        };
+
+        double step = C.step_init;
+        double dec;
+        double J = eval_j(al_p, false, dec);
+        eval_grad();
+        int evals = 1, accepts = 0;
+        double J_prev = J;
+        for (int it = 0; it < C.max_inner_iters; ++it) {
+            bool accepted = false;
+            int bt = 0;
+            while (bt < 20) {
+                for (int i = tid; i < N; i += TS) an_p[i] = fmin(HI[i], fmax(LO[i], al_p[i] - step * GR[i]));
+                __syncthreads();
+                const double Jn = eval_j(an_p, true, dec);
+                ++evals;
+                if (Jn <= J + C.armijo_c * dec) {
+                    double* t = al_p; al_p = an_p; an_p = t;       // α := α_trial (uniform swap)
+                    eval_grad();
+                    J = Jn;
+                    accepted = true;
+                    ++accepts;
+                    break;
+                }
+                step *= 0.5;
+                bt++;
+                if (step < C.step_min) break;
+            }
+            if (!accepted) break;
+            if (fabs(J_prev - J) < 1e-10) break;
+            J_prev = J;
+        }
+        if (tid == 0) {
+            if (p.evals) p.evals[(size_t)b * MO + outer] = evals;
+            if (p.accepts) p.accepts[(size_t)b * MO + outer] = accepts;
+        }
+    }
+}
+
+template <bool CL, bool MT>
+static hipError_t launch_s(const KParams& p, const StreamBufs& sb, hipStream_t st) {
+    hipLaunchKernelGGL((rl_stream_kernel<CL, MT>), dim3(p.B), dim3(TS), 0, st, p, sb);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st) {
+    if (p.N <= 0 || p.N > RL_STREAM_MAX_N) return hipErrorInvalidValue;
+    if (p.closed) return mintime ? launch_s<true, true>(p, sb, st) : launch_s<true, false>(p, sb, st);
+    return mintime ? launch_s<false, true>(p, sb, st) : launch_s<false, false>(p, sb, st);
+}
+
+}  // namespace rl

@@ -107,7 +107,9 @@ def test_kernel_variant_table():
     assert lib.rl_kernel_variant(187) == 4
     assert lib.rl_kernel_variant(2000) == 8
     assert lib.rl_kernel_variant(4096) == 8
-    assert lib.rl_kernel_variant(4097) == abi.RL_ETOOBIG
+    assert lib.rl_kernel_variant(4097) == 1          # large-N streaming kernel
+    assert lib.rl_kernel_variant(10000) == 1
+    assert lib.rl_kernel_variant((1 << 20) + 1) == abi.RL_ETOOBIG
 
 
 def test_compute_fails_loudly_without_gpu():

@@ -45,7 +45,7 @@ def compare_outputs(got: abi.Outputs, ref: abi.Outputs, mintime: bool, label: st
             np.testing.assert_array_equal(got.vpass_sweeps, ref.vpass_sweeps, err_msg=f"{label}.sweeps")
 
 
-GOLDEN = [c for c in O.manifest()["cases"] if c != "oval_n10000"]
+GOLDEN = list(O.manifest()["cases"])    # includes the N=10000 oval (streaming kernel)
 
 
 @pytest.mark.parametrize("name", GOLDEN)
@@ -184,6 +184,38 @@ def test_reference_shaped_calls():
     assert e.raceline.shape == (0, 2) and e.lap_time == 0.0
 
 
+@pytest.mark.parametrize("closed", [True, False])
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 64, 1000, 1025, 2047, 4097])
+def test_streaming_kernel_vs_oracle(N, closed, monkeypatch):
+    """The large-N streaming kernel (forced for small N too) against the oracle."""
+    _lib_or_skip()
+    monkeypatch.setenv("RL_FORCE_STREAM", "1")
+    rng = np.random.default_rng(N + 7)
+    prob = _synthetic(N, closed, rng)
+    cfg = abi.default_cfg()
+    cfg.max_outer_iters = 3
+    cfg.max_inner_iters = 20
+    mc, mt = raceline.optimize_batch(prob, cfg, [0, 9], 2)
+    omc, omt = O.run_oracle(prob, cfg, seeds=[0, 9], B=2)
+    compare_outputs(mc, omc, False, f"stream N{N}.mc")
+    compare_outputs(mt, omt, True, f"stream N{N}.mt")
+
+
+def test_streaming_kernel_golden_tracks(monkeypatch):
+    """Streaming kernel on a default track and on N=2000 (vs the reference fixtures)."""
+    _lib_or_skip()
+    monkeypatch.setenv("RL_FORCE_STREAM", "1")
+    for name in ("track_training_map", "cmap1_n2000"):
+        case = O.load_case(name)
+        prob, cfg = O.case_problem(case), O.case_cfg(case)
+        mc, mt = raceline.optimize_batch(prob, cfg, None, 1)
+        for f in abi.OUT_F64:
+            col_close(mc.__dict__[f][0], case[f"mc_{f}"], f"stream {name}.mc_{f}")
+        for f in abi.OUT_F64_MT:
+            col_close(mt.__dict__[f][0], case[f"mt_{f}"], f"stream {name}.mt_{f}")
+        assert abs(mt.lap[0] - float(case["mt_lap"])) / float(case["mt_lap"]) <= REL
+
+
 def test_errors_fail_loudly():
     _lib_or_skip()
     case = O.load_case("track_training_map")
@@ -191,7 +223,7 @@ def test_errors_fail_loudly():
     cfg = O.case_cfg(case)
     with pytest.raises(raceline.RacelineError):
         raceline.optimize_batch(prob, [cfg, cfg, cfg], None, 2)          # n_cfg not 1 or B
-    big = abi.Problem(center=np.zeros((5000, 2)), L=100.0, inner_seg=prob.inner_seg, outer_seg=prob.outer_seg)
+    big = abi.Problem(center=np.zeros(((1 << 20) + 1, 2)), L=100.0, inner_seg=prob.inner_seg, outer_seg=prob.outer_seg)
     with pytest.raises(raceline.RacelineError) as ei:
         raceline.optimize_batch(big, cfg, None, 1)
     assert ei.value.code == abi.RL_ETOOBIG
