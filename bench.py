@@ -32,6 +32,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 from practice_path_planning_for_formula_student_driverless_amd import abi, raceline  # noqa: E402
+from practice_path_planning_for_formula_student_driverless_amd import distributed as D  # noqa: E402
 
 # fp64 peak on MI355X (AMD spec: FP64 vector = FP64 dense matrix = 78.6 TFLOP/s;
 # the path runs on the fp64 VALU, there is no MFMA-shaped contraction in it).
@@ -94,6 +95,101 @@ def cpu_baseline(prob, cfg, budget_s: float = 12.0, max_inst: int = 64):
                       f"{dt:.1f} s, one thread"}
 
 
+def run_c4(world, rank, local, dev, dist):
+    """C4: 7 bundled tracks x 512 (mu, P_max_W, lambda_smooth) points, min-curv + min-time.
+    Items are sharded track-major over ranks; one plan per track, all plans on
+    concurrent HIP streams; laps gathered to rank 0."""
+    import torch
+
+    groups = D.c4_shard(world, rank)
+    base = load_problem("track_training_map")[2]
+    cfgs = D.c4_cfgs(base)
+    plans, meta = [], []
+    for t, ks in groups.items():
+        case, prob, _ = load_problem("track_" + D.C4_TRACKS[t])
+        plans.append(raceline.Plan(prob, [cfgs[k] for k in ks], B=len(ks),
+                                   modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, device=local))
+        meta.append((t, ks, prob))
+    streams = [torch.cuda.Stream(device=dev) for _ in plans]
+
+    def launch():
+        for pl, st in zip(plans, streams):
+            pl.run(st.cuda_stream)
+        for st in streams:
+            st.synchronize()
+
+    launch()
+    if dist is not None:
+        dist.barrier()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        launch()
+    dt = (time.perf_counter() - t0) / reps
+    n_inst = sum(len(ks) for _, ks, _ in meta)
+    laps = np.concatenate([pl.fetch()[1].lap for pl in plans])
+    # parity spot check (outside timing): first sweep point of this rank's first track vs the oracle
+    import oracle_lib as O
+    t, ks, prob = meta[0]
+    _, omt = O.run_oracle(prob, [cfgs[ks[0]]], B=1, modes=(False, True))
+    lap_delta = float(abs(laps[0] - omt.lap[0]))
+    stats = torch.tensor([dt, float(n_inst), lap_delta], dtype=torch.float64, device=dev)
+    if dist is not None:
+        per = D.pad_to(3584, world)
+        lt = torch.zeros(per, dtype=torch.float64, device=dev)
+        lt[:len(laps)] = torch.from_numpy(laps)
+        got = D.gather_to_root({"laps": lt, "stats": stats}, world, rank)
+        if rank != 0:
+            return None
+        all_stats = torch.stack(got["stats"]).cpu().numpy()
+        dt, n_inst, lap_delta = float(all_stats[:, 0].max()), int(all_stats[:, 1].sum()), float(all_stats[:, 2].max())
+        laps = np.concatenate([g.cpu().numpy()[: int(s[1])] for g, s in zip(got["laps"], all_stats)])
+    for pl in plans:
+        pl.close()
+    return {"instances": int(n_inst), "modes": "min-curv + min-time", "ms": round(dt * 1e3, 3),
+            "tracks_per_s": round(n_inst / dt, 1), "outer_iters_per_s": round(2 * 14 * n_inst / dt, 1),
+            "lap_min_s": float(laps.min()), "lap_max_s": float(laps.max()),
+            "lap_delta_vs_oracle_s": lap_delta}
+
+
+def run_c5(world, rank, local, dev, dist):
+    """C5: synthetic oval N=10000 (streaming kernel, HBM-bound), 1024 seeds per rank, min-curv."""
+    import torch
+
+    case, prob, cfg = load_problem("oval_n10000")
+    B = 1024
+    s, _ = D.shard_range(world * B, world, rank)
+    plan = raceline.Plan(prob, cfg, seeds=np.arange(s, s + B, dtype=np.uint64), B=B,
+                         modes=abi.RL_MODE_MINCURV, device=local)
+    plan.run()
+    mc, _ = plan.fetch()
+    if dist is not None:
+        dist.barrier()
+    ms = []
+    for _ in range(2):
+        plan.run()
+        ms.append(plan.kernel_ms(1))
+    k_ms = float(np.mean(ms))
+    E_k = float(mc.evals.mean())
+    Eseg = prob.inner_seg.shape[0] + prob.outer_seg.shape[0]
+    by = B * 14 * bytes_per_outer(prob.N, E_k, Eseg)
+    rel = float(np.max(np.abs(mc.x[0] - case["mc_x"])) / np.max(np.abs(case["mc_x"]))) if s == 0 else 0.0
+    plan.close()
+    st = torch.tensor([k_ms, rel], dtype=torch.float64, device=dev)
+    if dist is not None:
+        got = D.gather_to_root({"st": st}, world, rank)
+        if rank != 0:
+            return None
+        arr = torch.stack(got["st"]).cpu().numpy()
+        k_ms, rel = float(arr[:, 0].max()), float(arr[:, 1].max())
+    return {"instances": world * B, "N": prob.N, "kernel_ms": round(k_ms, 3),
+            "outer_iters_per_s": round(world * B * 14 / (k_ms * 1e-3), 1), "evals_per_outer": E_k,
+            "roofline": {"bound": "hbm", "achieved": round(by / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(by / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "model": "SURVEY §8d streaming bytes N*(80*E_k+224)+32*E per outer"},
+            "seed0_vs_reference_max_rel_err": rel}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,9 +230,6 @@ def main():
     res = {k: torch.empty((B, N), **f64) for k in ("x", "y", "kappa", "alpha_last")}
     res["evals"] = torch.empty((B, MO), dtype=torch.int32, device=dev)
     plan.bind_device_outputs(abi.RL_MODE_MINCURV, {k: v.data_ptr() for k, v in res.items()})
-    gathered = None
-    if world > 1 and rank == 0:
-        gathered = {k: [torch.empty_like(v) for _ in range(world)] for k, v in res.items()}
 
     stream = torch.cuda.Stream(device=dev)
 
@@ -144,8 +237,7 @@ def main():
         plan.run(stream.cuda_stream)
         if world > 1:
             with torch.cuda.stream(stream):
-                for k, v in res.items():
-                    dist.gather(v, gathered[k] if rank == 0 else None, dst=0)
+                D.gather_to_root(res, world, rank)     # RCCL gather over xGMI (only collective)
 
     for _ in range(args.warmup):
         step()
@@ -174,6 +266,8 @@ def main():
     value = total_outer / elapsed
     tracks_per_s = world * B * args.steps / elapsed
 
+    c4 = None if args.no_extras else run_c4(world, rank, local, dev, dist)
+    c5 = None if args.no_extras else run_c5(world, rank, local, dev, dist)
     if rank != 0:
         plan.close()
         if dist is not None:
@@ -237,6 +331,10 @@ def main():
         }
         pl3.close()
 
+    if c4 is not None:
+        extras["c4_sweep_7tracks_x_512"] = c4
+    if c5 is not None:
+        extras["c5_oval_n10000"] = c5
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(prob, cfg)

@@ -1,0 +1,86 @@
+"""Multi-GPU plumbing for batched raceline optimisation.
+
+Instances (α-seeds, cfg sweep points, tracks) are independent, so the batch is
+sharded across ranks with no data-path collective (weak scaling); a single
+instance is never split.  The only collective is the final gather of results
+to rank 0 over RCCL (torch.distributed backend "nccl" on ROCm) — or gloo on CPU
+for the tests.  One process per GPU, launched by torch.distributed.run.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+
+
+def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous block [start, end) of `total` items for `rank` (sizes differ by <= 1)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    base, rem = divmod(total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def gather_to_root(tensors: Dict[str, "object"], world: int, rank: int, group=None):
+    """dist.gather every tensor of `tensors` to rank 0.  Shapes must match across
+    ranks (pad shards to the same size).  Returns {name: [tensor per rank]} on rank 0,
+    None elsewhere.  With the nccl backend this is RCCL over xGMI, device to device."""
+    import torch
+    import torch.distributed as dist
+
+    out = {} if rank == 0 else None
+    for name, t in tensors.items():
+        lst = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+        dist.gather(t, lst, dst=0, group=group)
+        if rank == 0:
+            out[name] = lst
+    return out
+
+
+# ----------------------------------------------------------------- C4 sweep
+C4_TRACKS = ["training_map", "competition_map1", "competition_map2", "competition_map3",
+             "competition_map_testday1", "competition_map_testday2", "competition_map_testday3"]
+
+
+def c4_grid() -> List[Tuple[float, float, float]]:
+    """mu in linspace(0.9,1.5,8), P_max_W in linspace(40kW,120kW,8),
+    lambda_smooth in logspace(4e-4, 6.4e-3, 8) -> 512 points (mu-major)."""
+    mus = np.linspace(0.9, 1.5, 8)
+    Ps = np.linspace(40000.0, 120000.0, 8)
+    lams = np.geomspace(4e-4, 6.4e-3, 8)
+    return [(float(m), float(P), float(l)) for m in mus for P in Ps for l in lams]
+
+
+def c4_cfgs(base: abi.RlCfg) -> List[abi.RlCfg]:
+    """512 cfgs; a_total_max = 9.81*mu recomputed per point (ref:102 quirk)."""
+    out = []
+    for mu, P, lam in c4_grid():
+        c = abi.RlCfg.from_dict(base.to_dict())
+        abi.set_mu(c, mu)
+        c.P_max_W = P
+        c.lambda_smooth = lam
+        out.append(c)
+    return out
+
+
+def c4_items(n_tracks: int = 7, n_points: int = 512) -> List[Tuple[int, int]]:
+    """Track-major (track, sweep point) items: 7 x 512 = 3584."""
+    return [(t, k) for t in range(n_tracks) for k in range(n_points)]
+
+
+def c4_shard(world: int, rank: int, n_tracks: int = 7, n_points: int = 512) -> Dict[int, List[int]]:
+    """Rank's share of the C4 items grouped by track: {track: [sweep point indices]}."""
+    items = c4_items(n_tracks, n_points)
+    s, e = shard_range(len(items), world, rank)
+    groups: Dict[int, List[int]] = {}
+    for t, k in items[s:e]:
+        groups.setdefault(t, []).append(k)
+    return groups
+
+
+def pad_to(n: int, world: int) -> int:
+    return int(math.ceil(n / world))
