@@ -419,4 +419,9 @@ int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const 
     return rc;
 }
 
+#ifdef RL_STAMPS
+// diagnostic builds only: per-phase cycle totals of the last launch (see rl_kernels.hip)
+int rl_debug_stamps(unsigned long long* host, int nblocks) { return rl::debug_stamps(host, nblocks); }
+#endif
+
 }  // extern "C"

@@ -38,5 +38,8 @@ int pick_k(int N);
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
 // large-N variant: one 1024-thread workgroup per instance, state in HBM
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st);
+#ifdef RL_STAMPS
+int debug_stamps(unsigned long long* host, int nblocks);
+#endif
 
 }  // namespace rl

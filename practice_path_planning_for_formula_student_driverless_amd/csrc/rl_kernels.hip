@@ -37,6 +37,22 @@ namespace rl {
 
 constexpr int CK = 4;   // corridor sub-chunk (samples per ray-scan pass)
 
+// Diagnostic build only (-DRL_STAMPS=1): per-phase s_memtime totals of each
+// workgroup's wave 0, written to a device array no other code reads.
+#ifdef RL_STAMPS
+__device__ unsigned long long rl_dbg_stamps[16384][8];
+#define RL_STAMP(slot)                                              \
+    do {                                                            \
+        __builtin_amdgcn_sched_barrier(0);                          \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();       \
+        st_acc[slot] += t_ - st_last;                               \
+        st_last = t_;                                               \
+        __builtin_amdgcn_sched_barrier(0);                          \
+    } while (0)
+#else
+#define RL_STAMP(slot) do {} while (0)
+#endif
+
 // ------------------------------------------------------------ wave primitives
 template <int CTRL>
 __device__ __forceinline__ double dpp(double x) {
@@ -142,6 +158,10 @@ template <int K, int T, bool CLOSED, bool MT>
 __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel(KParams p) {
     constexpr int NW = T / 64;
     __shared__ Smem<K, T> sm;
+#ifdef RL_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int b = blockIdx.x;
@@ -631,6 +651,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     for (int k = 0; k < K; ++k) { al[k] = 0.0; gr[k] = 0.0; G2[k] = 0.0; }
 
     const int MO = C.max_outer_iters;
+    RL_STAMP(0);
     for (int outer = 0;; ++outer) {
         if (outer > 0 && active) {
             // update (ref:743-746 / 1027-1030): alpha_last, P += n*alpha, alpha_accum
@@ -648,6 +669,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #pragma unroll
         for (int k = 0; k < K; ++k) { al[k] = 0.0; gr[k] = 0.0; }   // ref:757 / 1041
         __syncthreads();
+        RL_STAMP(5);
         if (outer < MO) {
             // normals + corridor (ref:692-711 initially with the veh_width argument,
             // ref:746-756 after each update with cfg veh_width_m)
@@ -663,6 +685,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 }
             }
         }
+        RL_STAMP(1);
         double ka[K];
         if (MT || outer == MO) {
             // heading_curv_from_points_generic ref:595-620
@@ -758,6 +781,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 __syncthreads();   // vin (aliased with coef) fully consumed before coef is written
             }
         }
+        RL_STAMP(2);
         if (outer == MO) break;
 
         // precompute_lin_geom_generic ref:622-651 -> LDS (own entries only)
@@ -780,6 +804,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 sm.u.coef[1][k][tid] = make_double2(v ? n0 : 0.0, v ? w : 0.0);
             }
         }
+        RL_STAMP(3);
         // PGD + Armijo (ref:723-742 / 996-1026)
         double step = C.step_init;
         double dec;
@@ -821,8 +846,22 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             if (p.evals) p.evals[(size_t)b * MO + outer] = evals;
             if (p.accepts) p.accepts[(size_t)b * MO + outer] = accepts;
         }
+        RL_STAMP(4);
     }
+#ifdef RL_STAMPS
+    RL_STAMP(6);
+    if (tid == 0 && b < 16384) {
+        for (int i = 0; i < 8; ++i) rl_dbg_stamps[b][i] = st_acc[i];
+    }
+#endif
 }
+
+#ifdef RL_STAMPS
+int debug_stamps(unsigned long long* host, int nblocks) {
+    if (nblocks > 16384) nblocks = 16384;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_stamps), sizeof(unsigned long long) * 8 * nblocks) == hipSuccess ? 0 : -3;
+}
+#endif
 
 // ------------------------------------------------------------------ launcher
 template <int K, int T, bool CL, bool MT>
