@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include "rl_abi.h"
+#include "rl_corridor.h"
 #include "rl_device.h"
 #include "rl_kernels.h"
 #include "rl_math.h"
@@ -294,117 +295,24 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             if (k < cnt) { NX[i] = ox; NY[i] = oy; }
         }
     };
-    // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin), CK samples at a time
+    // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin), CK samples
+    // at a time through the per-lane candidate scan of rl_corridor.h
     auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
-        const SegRec* __restrict__ S = p.seg;
-        const int Ei = p.Ei, Ee = p.Ei + p.Eo;
 #pragma unroll
         for (int c = 0; c < K; c += CK) {
-            double qx[CK], qy[CK], ux[CK], uy[CK];
-            double bpi[CK], bni[CK], bpo[CK], bno[CK];
+            double qx[CK], qy[CK], ux[CK], uy[CK], lc[CK], hc[CK];
+            bool act[CK];
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
                 const int i = own(c + k);
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
-                bpi[k] = bni[k] = bpo[k] = bno[k] = INFINITY;
+                act[k] = c + k < cnt;
             }
-            // rayToRingDistance ref:491-500 over rayIntersectSegment ref:478-490, both
-            // directions at once: dir=-n gives den'=-den, t'=-t, u'=u bit-exactly
-            auto scan = [&](int e0, int e1, double (&bp)[CK], double (&bn)[CK]) RL_AI {
-                for (int e = e0; e < e1; ++e) {
-                    const SegRec s = S[e];
-#pragma unroll
-                    for (int k = 0; k < CK; ++k) {
-                        double den = ux[k] * (-s.vy) + uy[k] * (s.vx);
-                        double ax = s.x0 - qx[k], ay = s.y0 - qy[k];
-                        double nu = ux[k] * ay - uy[k] * ax;          // u = nu * (1/den)
-                        // conservative exact pretest: skip the division unless u can
-                        // land in [-1e-12, 1+1e-12] (u carries <= 2 roundings)
-                        const double ad = fabs(den), anu = fabs(nu);
-                        const bool same = (nu < 0) == (den < 0);
-                        const bool cand = !(ad < 1e-15) && (anu <= 1.0000001 * ad) && (same || anu <= 4e-12 * ad);
-                        if (cand) {
-                            double inv = 1.0 / den;
-                            double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
-                            double u = nu * inv;
-                            if (u >= -1e-12 && u <= 1.0 + 1e-12) {
-                                if (t > 0.0 && t < bp[k]) bp[k] = t;
-                                double tn = -t;
-                                if (tn > 0.0 && tn < bn[k]) bn[k] = tn;
-                            }
-                        }
-                    }
-                }
-            };
-            scan(0, Ei, bpi, bni);
-            scan(Ei, Ee, bpo, bno);
-            // minDistanceToSegments_global fallback (ref:501-512) where a ray missed
-            // Two passes: an upper bound ub >= min distance from the segment start
-            // points, then the exact reference expression only for segments whose
-            // lower bound |P-mid| - half_length does not exceed ub.
-            auto mindist = [&](int e0, int e1, double (&md)[CK]) RL_AI {
-                double ub2[CK];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) ub2[k] = INFINITY;
-                for (int e = e0; e < e1; ++e) {
-                    const SegRec s = S[e];
-#pragma unroll
-                    for (int k = 0; k < CK; ++k) {
-                        double dx = qx[k] - s.x0, dy = qy[k] - s.y0;
-                        ub2[k] = fmin(ub2[k], dx * dx + dy * dy);
-                    }
-                }
-                double lim[CK];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) lim[k] = sqrt(ub2[k]) * (1.0 + 1e-9) + 1e-12;
-                for (int e = e0; e < e1; ++e) {
-                    const SegRec s = S[e];
-#pragma unroll
-                    for (int k = 0; k < CK; ++k) {
-                        double mx = qx[k] - s.mx, my = qy[k] - s.my;
-                        double r = lim[k] + s.hr;
-                        if (!(mx * mx + my * my > r * r)) {
-                            double apx = qx[k] - s.x0, apy = qy[k] - s.y0;
-                            double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
-                            double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
-                            md[k] = smin(md[k], hypot_ref(qx[k] - Qx, qy[k] - Qy));
-                        }
-                    }
-                }
-            };
-            bool need_i = false, need_o = false;
+            corridor_bounds<CK>(p.seg, p.Ei, p.Eo, qx, qy, ux, uy, act, guard, lc, hc);
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
-                if (c + k < cnt) {
-                    need_i |= !isfinite(bpi[k]) || !isfinite(bni[k]);
-                    need_o |= !isfinite(bpo[k]) || !isfinite(bno[k]);
-                }
-            }
-            double mdi[CK], mdo[CK];
-#pragma unroll
-            for (int k = 0; k < CK; ++k) mdi[k] = mdo[k] = INFINITY;
-            if (__any(need_i)) mindist(0, Ei, mdi);
-            if (__any(need_o)) mindist(Ei, Ee, mdo);
-#pragma unroll
-            for (int k = 0; k < CK; ++k) {
-                // safe_ray ref:694-699
-                double spi = bpi[k], sni = bni[k], spo = bpo[k], sno = bno[k];
-                if (!isfinite(spi)) spi = mdi[k];
-                if (!isfinite(spi)) spi = 0.0;
-                if (!isfinite(sni)) sni = mdi[k];
-                if (!isfinite(sni)) sni = 0.0;
-                if (!isfinite(spo)) spo = mdo[k];
-                if (!isfinite(spo)) spo = 0.0;
-                if (!isfinite(sno)) sno = mdo[k];
-                if (!isfinite(sno)) sno = 0.0;
-                double dpos = smin(smax(0.0, spi), smax(0.0, spo));
-                double dneg = smin(smax(0.0, sni), smax(0.0, sno));
-                double hk = smax(0.0, dpos - guard);
-                double lk = -smax(0.0, dneg - guard);
-                if (!isfinite(hk)) hk = 0.0;
-                if (!isfinite(lk)) lk = 0.0;
-                hi[c + k] = (c + k < cnt) ? hk : 0.0;
-                lo[c + k] = (c + k < cnt) ? lk : 0.0;
+                hi[c + k] = act[k] ? hc[k] : 0.0;
+                lo[c + k] = act[k] ? lc[k] : 0.0;
             }
         }
     };

@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "rl_abi.h"
+#include "rl_corridor.h"
 #include "rl_device.h"
 #include "rl_kernels.h"
 #include "rl_math.h"
@@ -156,64 +157,14 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
         NX[i] = ox;
         NY[i] = oy;
     };
-    // corridor (ref:694-711 / 749-756) at sample i, both ray directions per segment
-    const SegRec* __restrict__ S = p.seg;
+    // corridor (ref:694-711 / 749-756) at sample i via the per-lane candidate scan
     auto corridor_at = [&](int i, double guard) {
-        const double qx = X[i], qy = Y[i], ux = NX[i], uy = NY[i];
-        double bp[2] = {INFINITY, INFINITY}, bn[2] = {INFINITY, INFINITY}, md[2] = {INFINITY, INFINITY};
-        const int e_lo[2] = {0, p.Ei}, e_hi[2] = {p.Ei, p.Ei + p.Eo};
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            for (int e = e_lo[r]; e < e_hi[r]; ++e) {
-                const SegRec s = S[e];
-                double den = ux * (-s.vy) + uy * (s.vx);
-                double ax = s.x0 - qx, ay = s.y0 - qy;
-                double nu = ux * ay - uy * ax;
-                const double ad = fabs(den), anu = fabs(nu);
-                const bool same = (nu < 0) == (den < 0);
-                if (!(ad < 1e-15) && (anu <= 1.0000001 * ad) && (same || anu <= 4e-12 * ad)) {
-                    double inv = 1.0 / den;
-                    double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
-                    double u = nu * inv;
-                    if (u >= -1e-12 && u <= 1.0 + 1e-12) {
-                        if (t > 0.0 && t < bp[r]) bp[r] = t;
-                        double tn = -t;
-                        if (tn > 0.0 && tn < bn[r]) bn[r] = tn;
-                    }
-                }
-            }
-            if (!isfinite(bp[r]) || !isfinite(bn[r])) {   // minDistanceToSegments_global ref:501-512
-                double ub2 = INFINITY;
-                for (int e = e_lo[r]; e < e_hi[r]; ++e) {
-                    double dx = qx - S[e].x0, dy = qy - S[e].y0;
-                    ub2 = fmin(ub2, dx * dx + dy * dy);
-                }
-                const double lim = sqrt(ub2) * (1.0 + 1e-9) + 1e-12;
-                for (int e = e_lo[r]; e < e_hi[r]; ++e) {
-                    const SegRec s = S[e];
-                    double mx = qx - s.mx, my = qy - s.my, rr = lim + s.hr;
-                    if (!(mx * mx + my * my > rr * rr)) {
-                        double apx = qx - s.x0, apy = qy - s.y0;
-                        double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
-                        double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
-                        md[r] = smin(md[r], hypot_ref(qx - Qx, qy - Qy));
-                    }
-                }
-            }
-        }
-        auto safe = [](double t, double m) {
-            if (!isfinite(t)) t = m;
-            if (!isfinite(t)) t = 0.0;
-            return smax(0.0, t);
-        };
-        double dpos = smin(safe(bp[0], md[0]), safe(bp[1], md[1]));
-        double dneg = smin(safe(bn[0], md[0]), safe(bn[1], md[1]));
-        double hk = smax(0.0, dpos - guard);
-        double lk = -smax(0.0, dneg - guard);
-        if (!isfinite(hk)) hk = 0.0;
-        if (!isfinite(lk)) lk = 0.0;
-        HI[i] = hk;
-        LO[i] = lk;
+        const double qx[1] = {X[i]}, qy[1] = {Y[i]}, ux[1] = {NX[i]}, uy[1] = {NY[i]};
+        const bool act[1] = {true};
+        double lk[1], hk[1];
+        corridor_bounds<1>(p.seg, p.Ei, p.Eo, qx, qy, ux, uy, act, guard, lk, hk);
+        HI[i] = hk[0];
+        LO[i] = lk[0];
     };
     // difference operators at sample i (DiffOps / DiffOpsOpen ref:545-579)
     auto d1_at = [&](int i, double am, double a0, double ap) -> double {
