@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -31,21 +33,66 @@ int fail(int code, const std::string& msg) {
 // std::max (ref:506 uses std::max(1e-30, ...))
 inline double smax_h(double a, double b) { return (a < b) ? b : a; }
 
-// Segment records from [E][4] (x0,y0,x1,y1); vx,vy,denom exactly as the reference
-// computes them (ref:482, 505-506).  mx,my,hr for conservative culling.
-void make_segrecs(const double* s, int E, std::vector<rl::SegRec>& out) {
+// Segment record from (x0,y0,x1,y1); vx,vy,denom exactly as the reference computes
+// them (ref:482, 505-506).  mx,my,hr for conservative culling.
+rl::SegRec make_segrec(const double* q) {
+    rl::SegRec r;
+    r.x0 = q[0];
+    r.y0 = q[1];
+    r.vx = q[2] - q[0];
+    r.vy = q[3] - q[1];
+    r.denom = smax_h(1e-30, r.vx * r.vx + r.vy * r.vy);
+    r.mx = 0.5 * (q[0] + q[2]);
+    r.my = 0.5 * (q[1] + q[3]);
+    r.hr = 0.5 * std::sqrt(r.vx * r.vx + r.vy * r.vy) * (1.0 + 1e-9) + 1e-12;
+    return r;
+}
+
+// Host image of one ring in the entry-stream form of rl_corridor.h: the vertices of
+// each chain of consecutive segments (a segment starts a new chain unless its start
+// equals the previous segment's end bit for bit), entry v holding the record of the
+// segment that ends at v; padded to blocks of 32 with NaN entries.
+struct RingHost {
+    std::vector<double> vtx;        // [M][2]
+    std::vector<rl::SegRec> rec;    // [M]
+    std::vector<uint32_t> flag;     // [M/32]
+    int M = 0, E = 0;
+    double dl0 = 0;
+};
+
+RingHost make_ring(const double* s, int E) {
+    RingHost R;
+    R.E = E;
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    rl::SegRec dummy;
+    dummy.x0 = dummy.y0 = dummy.vx = dummy.vy = dummy.mx = dummy.my = dummy.hr = nan;
+    dummy.denom = 1.0;
+    std::vector<char> ends;
+    auto push = [&](double x, double y, const rl::SegRec& r, bool end) {
+        R.vtx.push_back(x);
+        R.vtx.push_back(y);
+        R.rec.push_back(r);
+        ends.push_back(end);
+    };
+    double vmax = 0, rv = 0;
     for (int e = 0; e < E; ++e) {
-        rl::SegRec r;
-        r.x0 = s[4 * e];
-        r.y0 = s[4 * e + 1];
-        r.vx = s[4 * e + 2] - s[4 * e];
-        r.vy = s[4 * e + 3] - s[4 * e + 1];
-        r.denom = smax_h(1e-30, r.vx * r.vx + r.vy * r.vy);
-        r.mx = 0.5 * (s[4 * e] + s[4 * e + 2]);
-        r.my = 0.5 * (s[4 * e + 1] + s[4 * e + 3]);
-        r.hr = 0.5 * std::sqrt(r.vx * r.vx + r.vy * r.vy) * (1.0 + 1e-9) + 1e-12;
-        out.push_back(r);
+        const double* q = s + 4 * e;
+        if (e == 0 || !(q[0] == s[4 * e - 2] && q[1] == s[4 * e - 1])) push(q[0], q[1], dummy, false);
+        const rl::SegRec r = make_segrec(q);
+        push(q[2], q[3], r, true);
+        vmax = std::max(vmax, std::fabs(r.vx) + std::fabs(r.vy));
+        rv = std::max(rv, std::max(std::fabs(q[0]) + std::fabs(q[1]), std::fabs(q[2]) + std::fabs(q[3])));
     }
+    while (ends.size() % 32) push(nan, nan, dummy, false);
+    R.M = (int)ends.size();
+    R.flag.assign(R.M / 32, 0u);
+    for (int v = 0; v < R.M; ++v)
+        if (ends[v]) R.flag[v / 32] |= 0x80000000u >> (v % 32);
+    // NaN/inf coordinates make dl0 non-finite: every pair is then a candidate and the
+    // exact expressions propagate the values like the reference
+    R.dl0 = 4e-12 * (1.0 + vmax) + 4e-15 * rv;
+    if (!(vmax == vmax) || !(rv == rv)) R.dl0 = nan;
+    return R;
 }
 
 struct ModeBufs {
@@ -73,7 +120,11 @@ struct rl_plan {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran = false;
     double* d_center = nullptr;
-    rl::SegRec* d_seg = nullptr;
+    double* d_vtx = nullptr;
+    rl::SegRec* d_rec = nullptr;
+    uint32_t* d_flag = nullptr;
+    int ring_M[2] = {0, 0};
+    double ring_dl0[2] = {0, 0};
     rl_cfg* d_cfg = nullptr;
     uint64_t* d_seeds = nullptr;
     ModeBufs mb[2];
@@ -233,17 +284,26 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
         if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
 
     const size_t N = (size_t)std::max(p->N, 1), BN = (size_t)B * N;
-    std::vector<rl::SegRec> segs;
-    make_segrecs(prob->inner_seg, prob->Ei, segs);
-    make_segrecs(prob->outer_seg, prob->Eo, segs);
-    if ((rc = p->alloc(&p->d_center, 2 * N)) || (rc = p->alloc(&p->d_seg, segs.size())) ||
+    RingHost rh[2] = {make_ring(prob->inner_seg, prob->Ei), make_ring(prob->outer_seg, prob->Eo)};
+    const size_t Mt = (size_t)rh[0].M + rh[1].M;
+    for (int r = 0; r < 2; ++r) { p->ring_M[r] = rh[r].M; p->ring_dl0[r] = rh[r].dl0; }
+    if ((rc = p->alloc(&p->d_center, 2 * N)) || (rc = p->alloc(&p->d_vtx, 2 * Mt)) ||
+        (rc = p->alloc(&p->d_rec, Mt)) || (rc = p->alloc(&p->d_flag, Mt / 32)) ||
         (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
         return cleanup(rc);
     hipStream_t st = p->own_stream;
     if (p->N > 0 && hipMemcpyAsync(p->d_center, prob->center_xy, 2 * N * sizeof(double), hipMemcpyHostToDevice, st))
         return cleanup(fail(RL_EHIP, "upload center"));
-    if (!segs.empty() && hipMemcpyAsync(p->d_seg, segs.data(), segs.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st))
-        return cleanup(fail(RL_EHIP, "upload segments"));
+    for (int r = 0, off = 0; r < 2; off += rh[r].M, ++r) {
+        const RingHost& R = rh[r];
+        if (R.M == 0) continue;
+        if (hipMemcpyAsync(p->d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st))
+            return cleanup(fail(RL_EHIP, "upload rings"));
+        // the copies read the host vectors: wait before they go out of scope
+        if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(RL_EHIP, "upload sync"));
+    }
     if (hipMemcpyAsync(p->d_cfg, cfg, (size_t)n_cfg * sizeof(rl_cfg), hipMemcpyHostToDevice, st))
         return cleanup(fail(RL_EHIP, "upload cfg"));
     std::vector<uint64_t> sd((size_t)B, 0);
@@ -300,7 +360,14 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         (void)BN;
         rl::KParams kp;
         kp.center = p->d_center;
-        kp.seg = p->d_seg;
+        for (int r = 0, off = 0; r < 2; off += p->ring_M[r], ++r) {
+            kp.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
+            kp.ring[r].rec = p->d_rec + off;
+            kp.ring[r].flag = p->d_flag + off / 32;
+            kp.ring[r].M = p->ring_M[r];
+            kp.ring[r].E = r == 0 ? p->Ei : p->Eo;
+            kp.ring[r].dl0 = p->ring_dl0[r];
+        }
         kp.cfg = p->d_cfg;
         kp.seeds = p->d_seeds;
         kp.x = mb.x; kp.y = mb.y; kp.heading = mb.heading; kp.kappa = mb.kappa;

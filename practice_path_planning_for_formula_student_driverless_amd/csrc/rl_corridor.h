@@ -3,19 +3,28 @@
 //   minDistanceToSegments_global ref:501-512, safe_ray ref:694-699,
 //   corridor blocks ref:701-711 / 749-756.
 //
-// For CK samples per lane (P, n), both rings:
-//   1. a uniform pass over blocks of 64 segments computes, per sample, the cheap
-//      pretest of the ray test (u numerator vs denominator) and sets a bit in a
-//      per-lane 64-bit candidate mask; it also tracks |P - S0|^2, an upper bound
-//      of the ring's point-to-segment distance;
-//   2. each lane then walks only ITS set bits (ctz loop, per-lane loads of the
-//      64-B segment record from L1) and evaluates the reference expressions
-//      exactly — the wave no longer runs the exact path for the union of all
-//      lanes' candidates;
-//   3. where a ray missed, the point-to-segment fallback does the same with the
-//      conservative lower bound |P - mid| - half_len <= upper bound as filter.
+// Rings arrive as an ENTRY STREAM (built by rl_abi.cpp make_ring): the vertices of
+// each chain of segments in order, padded to blocks of 32 entries; entry v carries
+// the record of the segment that ENDS at v (flag bit set) or a dummy (chain start,
+// padding).  For CK samples (P, n) per lane:
+//   1. filter: per entry, the side of the ray line c_v = n x (V_v - P) (two fma with
+//      a per-sample constant, two compares); a segment is a candidate unless both its endpoints lie
+//      strictly on the same side by more than dl (see below).  The candidate bit
+//      shifts into a per-lane 32-bit word (w = 2w + cand, MSB = first entry);
+//   2. each lane walks only ITS candidates (clz loop; the CK samples' record loads
+//      issued together) and evaluates the reference expressions exactly;
+//   3. where a ray missed, the point-to-segment fallback: an upper bound ub from
+//      the walked candidates' endpoints, then the conservative lower bound
+//      |P - mid| - half_len <= ub as filter and the exact walk again.
 // The ±n rays share one test: d -> -d gives den' = -den, t' = -t, u' = u bit-exactly.
-// Every skipped pair provably cannot change the reference's minimum.
+//
+// Why skipping is exact: with C0, C1 the true sides of the two endpoints, the
+// reference's u = nu/den has nu = c0 up to rounding, den = (C0-C1) + eta with
+// |eta| <= 7e-16|v|, |nu_f - C| <= 4.5e-16 (|ax|+|ay|) and |c_f - C| <= 6e-16 (Rv+|qx|+|qy|).  If both c0, c1 > dl
+// (or both < -dl) with dl = 4e-12 (1 + Vmax) + 4e-15 (Rv + |qx|+|qy|)
+// (Vmax = max |vx|+|vy|, Rv = max |x|+|y| over the ring), then u < -1e-12
+// (|u| >= dl/|v| >= 4e-12), or u > 1 + 1e-12 ((u-1) >= (dl - 1.1e-15 R - 7e-16|v|)/|v|),
+// or the pair is near-parallel with |u| >> 1 — the reference rejects the pair.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -24,14 +33,30 @@
 
 namespace rl {
 
+// uniform (wave-invariant) reads of the ring streams go through the constant address
+// space so they become scalar (SMEM) loads; the kernel never writes these buffers
+typedef __attribute__((address_space(4))) const double cdbl;
+typedef __attribute__((address_space(4))) const uint32_t cu32;
+__device__ __forceinline__ cdbl* as_cdbl(const void* p) { return (cdbl*)p; }
+__device__ __forceinline__ cu32* as_cu32(const void* p) { return (cu32*)p; }
+
+// one ring in entry-stream form (device pointers); M is a multiple of 32
+struct RingDesc {
+    const double2* vtx;       // [M] entry vertex (NaN for padding)
+    const SegRec* rec;        // [M] record of the segment ending at the entry
+    const uint32_t* flag;     // [M/32] bit (31-j): entry 32b+j ends a segment
+    int32_t M, E;             // padded entry count, segment count
+    double dl0;               // 4e-12*(1+Vmax) + 4e-15*Rv
+};
+
 // exact rayIntersectSegment for +n and -n at once, folded into the running minima
-__device__ __forceinline__ void ray_exact(const SegRec& s, double qx, double qy, double ux, double uy,
-                                          double& bp, double& bn) {
-    double den = ux * (-s.vy) + uy * (s.vx);
+__device__ __forceinline__ void ray_exact(double x0, double y0, double vx, double vy, double qx, double qy,
+                                          double ux, double uy, double& bp, double& bn) {
+    double den = ux * (-vy) + uy * (vx);
     if (fabs(den) < 1e-15) return;
-    double ax = s.x0 - qx, ay = s.y0 - qy;
+    double ax = x0 - qx, ay = y0 - qy;
     double inv = 1.0 / den;
-    double t = (ax * (-s.vy) + ay * (s.vx)) * inv;
+    double t = (ax * (-vy) + ay * (vx)) * inv;
     double u = (ux * ay - uy * ax) * inv;
     if (u >= -1e-12 && u <= 1.0 + 1e-12) {
         if (t > 0.0 && t < bp) bp = t;       // ref:496-497
@@ -41,83 +66,157 @@ __device__ __forceinline__ void ray_exact(const SegRec& s, double qx, double qy,
 }
 
 // exact point-to-segment distance term of minDistanceToSegments_global (ref:504-509)
-__device__ __forceinline__ double seg_dist_exact(const SegRec& s, double qx, double qy) {
-    double apx = qx - s.x0, apy = qy - s.y0;
-    double t = sclamp((s.vx * apx + s.vy * apy) / s.denom, 0.0, 1.0);
-    double Qx = s.x0 + s.vx * t, Qy = s.y0 + s.vy * t;
+__device__ __forceinline__ double seg_dist_exact(double x0, double y0, double vx, double vy, double denom,
+                                                 double qx, double qy) {
+    double apx = qx - x0, apy = qy - y0;
+    double t = sclamp((vx * apx + vy * apy) / denom, 0.0, 1.0);
+    double Qx = x0 + vx * t, Qy = y0 + vy * t;
     return hypot_ref(qx - Qx, qy - Qy);
 }
 
-// one ring: rays (bp, bn) and, where needed, the point-to-segment fallback (md)
+// next candidate of each sample's word: entry offset j (0 if none), cleared from w
 template <int CK>
-__device__ __forceinline__ void ring_scan(const SegRec* __restrict__ S, int e0, int e1, const double (&qx)[CK],
-                                          const double (&qy)[CK], const double (&ux)[CK], const double (&uy)[CK],
-                                          const bool (&act)[CK], double (&bp)[CK], double (&bn)[CK],
-                                          double (&md)[CK]) {
-    double ub2[CK];
+__device__ __forceinline__ bool next_bits(uint32_t (&w)[CK], bool (&h)[CK], int (&j)[CK]) {
+    bool any = false;
 #pragma unroll
-    for (int k = 0; k < CK; ++k) { bp[k] = bn[k] = md[k] = INFINITY; ub2[k] = INFINITY; }
-    for (int b0 = e0; b0 < e1; b0 += 64) {
-        const int nb = min(64, e1 - b0);
-        unsigned long long m[CK];
+    for (int k = 0; k < CK; ++k) {
+        h[k] = w[k] != 0u;
+        j[k] = h[k] ? __clz(w[k]) : 0;
+        w[k] &= ~(0x80000000u >> j[k]);
+        any |= h[k];
+    }
+    return __any(any);
+}
+
+// one ring: ray distances along +n / -n with the safe_ray fallback applied
+// (ref:694-699), i.e. sp = safe(+n), sn = safe(-n), both >= 0
+template <int CK>
+__device__ __forceinline__ void ring_scan(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
+                                          const double (&ux)[CK], const double (&uy)[CK], const bool (&act)[CK],
+                                          double (&sp)[CK], double (&sn)[CK]) {
+    cdbl* V = as_cdbl(R.vtx);              // [M][2]
+    cdbl* SR = as_cdbl(R.rec);             // [M][8] SegRec fields (uniform reads)
+    cu32* F = as_cu32(R.flag);
+    const SegRec* __restrict__ S = R.rec;  // per-lane (divergent) reads
+    double dl[CK], g[CK], bp[CK], bn[CK], ub2[CK];
+    uint64_t pp[CK], pn[CK];       // side masks of the previous entry (wave lane masks, SGPR)
 #pragma unroll
-        for (int k = 0; k < CK; ++k) m[k] = 0ull;
-        for (int j = 0; j < nb; ++j) {
-            const double x0 = S[b0 + j].x0, y0 = S[b0 + j].y0, vx = S[b0 + j].vx, vy = S[b0 + j].vy;
+    for (int k = 0; k < CK; ++k) {
+        // c = n x (V - P) = ux*vy - uy*vx - g: |c_f - c| <= 6e-16 (Rv + |qx| + |qy|)
+        g[k] = ux[k] * qy[k] - uy[k] * qx[k];
+        dl[k] = R.dl0 + 4e-15 * (fabs(qx[k]) + fabs(qy[k]));
+        bp[k] = bn[k] = ub2[k] = INFINITY;
+        pp[k] = pn[k] = 0ull;
+    }
+    for (int b0 = 0; b0 < R.M; b0 += 32) {
+        uint32_t w[CK];
+#pragma unroll
+        for (int k = 0; k < CK; ++k) w[k] = 0u;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) {
+            const double vx = V[2 * (b0 + j)], vy = V[2 * (b0 + j) + 1];
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
-                const double ax = x0 - qx[k], ay = y0 - qy[k];
-                const double nu = ux[k] * ay - uy[k] * ax;          // u = nu * (1/den)
-                const double den = ux[k] * (-vy) + uy[k] * (vx);
-                const double ad = fabs(den), anu = fabs(nu);
-                // conservative: u can only land in [-1e-12, 1+1e-12] when this holds
-                const bool cand = !(ad < 1e-15) && (anu <= 1.0000001 * ad) && (((nu < 0) == (den < 0)) || anu <= 4e-12 * ad);
-                m[k] |= (unsigned long long)cand << j;
-                ub2[k] = fmin(ub2[k], ax * ax + ay * ay);
+                const double c = __builtin_fma(ux[k], vy, -__builtin_fma(uy[k], vx, g[k]));
+                const uint64_t P = __builtin_amdgcn_ballot_w64(c > dl[k]);
+                const uint64_t Q = __builtin_amdgcn_ballot_w64(c < -dl[k]);
+                const uint64_t cand = ~((P & pp[k]) | (Q & pn[k]));
+                w[k] = (w[k] << 1) | (uint32_t)__builtin_amdgcn_inverse_ballot_w64(cand);
+                pp[k] = P;
+                pn[k] = Q;
             }
         }
+        const uint32_t f = F[b0 >> 5];
 #pragma unroll
-        for (int k = 0; k < CK; ++k) {
-            unsigned long long mm = act[k] ? m[k] : 0ull;
-            while (mm) {
-                const int j = __builtin_ctzll(mm);
-                mm &= mm - 1;
-                ray_exact(S[b0 + j], qx[k], qy[k], ux[k], uy[k], bp[k], bn[k]);
+        for (int k = 0; k < CK; ++k) w[k] = act[k] ? (w[k] & f) : 0u;
+        bool h[CK];
+        int j[CK];
+        while (next_bits<CK>(w, h, j)) {
+            double x0[CK], y0[CK], sx[CK], sy[CK];
+#pragma unroll
+            for (int k = 0; k < CK; ++k) {
+                const SegRec* s = S + b0 + j[k];
+                x0[k] = s->x0; y0[k] = s->y0; sx[k] = s->vx; sy[k] = s->vy;
+            }
+#pragma unroll
+            for (int k = 0; k < CK; ++k) {
+                if (h[k]) {
+                    ray_exact(x0[k], y0[k], sx[k], sy[k], qx[k], qy[k], ux[k], uy[k], bp[k], bn[k]);
+                    // any segment endpoint bounds the point-to-segment minimum from above
+                    const double ax = qx[k] - x0[k], ay = qy[k] - y0[k];
+                    const double ex = ax - sx[k], ey = ay - sy[k];
+                    ub2[k] = fmin(ub2[k], fmin(ax * ax + ay * ay, ex * ex + ey * ey));
+                }
             }
         }
     }
-    // fallback only where a ray of this ring missed (safe_ray ref:696)
+    // minDistanceToSegments_global only where a ray of this ring missed (safe_ray ref:696)
+    double md[CK];
     bool need[CK];
-    bool any = false;
+    bool any_need = false, any_ub = false;
 #pragma unroll
-    for (int k = 0; k < CK; ++k) { need[k] = act[k] && (!isfinite(bp[k]) || !isfinite(bn[k])); any |= need[k]; }
-    if (!__any(any)) return;
-    double lim[CK];
+    for (int k = 0; k < CK; ++k) {
+        md[k] = INFINITY;
+        need[k] = act[k] && (!isfinite(bp[k]) || !isfinite(bn[k]));
+        any_need |= need[k];
+        any_ub |= need[k] && !isfinite(ub2[k]);
+    }
+    if (__any(any_need)) {
+        if (__any(any_ub)) {          // no candidate at all: bound from every vertex
+            for (int v = 0; v < R.M; ++v) {
+                const double vx = V[2 * v], vy = V[2 * v + 1];
 #pragma unroll
-    for (int k = 0; k < CK; ++k) lim[k] = sqrt(ub2[k]) * (1.0 + 1e-9) + 1e-12;
-    for (int b0 = e0; b0 < e1; b0 += 64) {
-        const int nb = min(64, e1 - b0);
-        unsigned long long m[CK];
-#pragma unroll
-        for (int k = 0; k < CK; ++k) m[k] = 0ull;
-        for (int j = 0; j < nb; ++j) {
-            const double mx = S[b0 + j].mx, my = S[b0 + j].my, hr = S[b0 + j].hr;
-#pragma unroll
-            for (int k = 0; k < CK; ++k) {
-                const double dx = qx[k] - mx, dy = qy[k] - my, r = lim[k] + hr;
-                const bool cand = need[k] && !(dx * dx + dy * dy > r * r);
-                m[k] |= (unsigned long long)cand << j;
+                for (int k = 0; k < CK; ++k) {
+                    const double dx = qx[k] - vx, dy = qy[k] - vy;
+                    ub2[k] = fmin(ub2[k], dx * dx + dy * dy);     // NaN padding is ignored
+                }
             }
         }
+        double lim[CK];
 #pragma unroll
-        for (int k = 0; k < CK; ++k) {
-            unsigned long long mm = m[k];
-            while (mm) {
-                const int j = __builtin_ctzll(mm);
-                mm &= mm - 1;
-                md[k] = smin(md[k], seg_dist_exact(S[b0 + j], qx[k], qy[k]));
+        for (int k = 0; k < CK; ++k) lim[k] = sqrt(ub2[k]) * (1.0 + 1e-9) + 1e-12;
+        for (int b0 = 0; b0 < R.M; b0 += 32) {
+            uint32_t w[CK];
+#pragma unroll
+            for (int k = 0; k < CK; ++k) w[k] = 0u;
+#pragma unroll 8
+            for (int j = 0; j < 32; ++j) {
+                cdbl* sr = SR + 8 * (b0 + j);
+                const double mx = sr[5], my = sr[6], hr = sr[7];
+#pragma unroll
+                for (int k = 0; k < CK; ++k) {
+                    const double dx = qx[k] - mx, dy = qy[k] - my, r = lim[k] + hr;
+                    const bool skip = dx * dx + dy * dy > r * r;
+                    w[k] = (w[k] << 1) | (uint32_t)!skip;
+                }
+            }
+            const uint32_t f = F[b0 >> 5];
+#pragma unroll
+            for (int k = 0; k < CK; ++k) w[k] = need[k] ? (w[k] & f) : 0u;
+            bool h[CK];
+            int j[CK];
+            while (next_bits<CK>(w, h, j)) {
+                double x0[CK], y0[CK], sx[CK], sy[CK], dn[CK];
+#pragma unroll
+                for (int k = 0; k < CK; ++k) {
+                    const SegRec* s = S + b0 + j[k];
+                    x0[k] = s->x0; y0[k] = s->y0; sx[k] = s->vx; sy[k] = s->vy; dn[k] = s->denom;
+                }
+#pragma unroll
+                for (int k = 0; k < CK; ++k)
+                    if (h[k]) md[k] = smin(md[k], seg_dist_exact(x0[k], y0[k], sx[k], sy[k], dn[k], qx[k], qy[k]));
             }
         }
+    }
+#pragma unroll
+    for (int k = 0; k < CK; ++k) {
+        double a = bp[k], b = bn[k];
+        if (!isfinite(a)) a = md[k];
+        if (!isfinite(a)) a = 0.0;
+        if (!isfinite(b)) b = md[k];
+        if (!isfinite(b)) b = 0.0;
+        sp[k] = smax(0.0, a);
+        sn[k] = smax(0.0, b);
     }
 }
 
@@ -125,27 +224,17 @@ __device__ __forceinline__ void ring_scan(const SegRec* __restrict__ S, int e0, 
 // Inactive samples (act false: padding of a ragged chunk) do no exact work; their
 // outputs are meaningless and the caller zeroes them.
 template <int CK>
-__device__ __forceinline__ void corridor_bounds(const SegRec* __restrict__ S, int Ei, int Eo, const double (&qx)[CK],
+__device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDesc& Ro, const double (&qx)[CK],
                                                 const double (&qy)[CK], const double (&ux)[CK],
                                                 const double (&uy)[CK], const bool (&act)[CK], double guard,
                                                 double (&lo)[CK], double (&hi)[CK]) {
-    double bpi[CK], bni[CK], mdi[CK], bpo[CK], bno[CK], mdo[CK];
-    ring_scan<CK>(S, 0, Ei, qx, qy, ux, uy, act, bpi, bni, mdi);
-    ring_scan<CK>(S, Ei, Ei + Eo, qx, qy, ux, uy, act, bpo, bno, mdo);
+    double spi[CK], sni[CK], spo[CK], sno[CK];
+    ring_scan<CK>(Ri, qx, qy, ux, uy, act, spi, sni);
+    ring_scan<CK>(Ro, qx, qy, ux, uy, act, spo, sno);
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
-        // safe_ray ref:694-699: ray distance, else point-to-segment minimum, else 0; max(0, .)
-        double spi = bpi[k], sni = bni[k], spo = bpo[k], sno = bno[k];
-        if (!isfinite(spi)) spi = mdi[k];
-        if (!isfinite(spi)) spi = 0.0;
-        if (!isfinite(sni)) sni = mdi[k];
-        if (!isfinite(sni)) sni = 0.0;
-        if (!isfinite(spo)) spo = mdo[k];
-        if (!isfinite(spo)) spo = 0.0;
-        if (!isfinite(sno)) sno = mdo[k];
-        if (!isfinite(sno)) sno = 0.0;
-        double dpos = smin(smax(0.0, spi), smax(0.0, spo));
-        double dneg = smin(smax(0.0, sni), smax(0.0, sno));
+        double dpos = smin(spi[k], spo[k]);
+        double dneg = smin(sni[k], sno[k]);
         double hk = smax(0.0, dpos - guard);
         double lk = -smax(0.0, dneg - guard);
         if (!isfinite(hk)) hk = 0.0;

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "rl_abi.h"
+#include "rl_corridor.h"
 #include "rl_device.h"
 
 namespace rl {
@@ -13,7 +14,7 @@ namespace rl {
 // instance-major [B][N]; x/y double as the path state P during the run.
 struct KParams {
     const double* center;      // [N][2]
-    const SegRec* seg;         // inner ring segments [Ei], then outer [Eo]
+    RingDesc ring[2];          // inner, outer ring as entry streams (rl_corridor.h)
     const rl_cfg* cfg;         // [ncfg]
     const uint64_t* seeds;     // [B] or nullptr
     double *x, *y, *heading, *kappa, *alpha_total, *alpha_last;

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                 act[k] = c + k < cnt;
             }
-            corridor_bounds<CK>(p.seg, p.Ei, p.Eo, qx, qy, ux, uy, act, guard, lc, hc);
+            corridor_bounds<CK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lc, hc);
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
                 hi[c + k] = act[k] ? hc[k] : 0.0;

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
         const double qx[1] = {X[i]}, qy[1] = {Y[i]}, ux[1] = {NX[i]}, uy[1] = {NY[i]};
         const bool act[1] = {true};
         double lk[1], hk[1];
-        corridor_bounds<1>(p.seg, p.Ei, p.Eo, qx, qy, ux, uy, act, guard, lk, hk);
+        corridor_bounds<1>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
         HI[i] = hk[0];
         LO[i] = lk[0];
     };

@@ -11,7 +11,8 @@ from practice_path_planning_for_formula_student_driverless_amd import abi
 
 libs = {}
 for p in sorted(glob.glob(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_*.so"))):
-    libs[os.path.basename(p)[6:-3]] = abi.load_library(p)
+    if not p.endswith("_stamps.so"):
+        libs[os.path.basename(p)[6:-3]] = abi.load_library(p)
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 
 def make_plan(lib, prob, cfg, B, modes):

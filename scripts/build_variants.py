@@ -8,9 +8,10 @@ VARIANTS = {
     "base": {},
     "k4t512w2": {"RL_MID_K": 4, "RL_MID_T": 512, "RL_MID_W": 2},
     "k4t512w4": {"RL_MID_K": 4, "RL_MID_T": 512, "RL_MID_W": 4},
+    "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
 }
 if __name__ == "__main__":
-    names = sys.argv[1:] or list(VARIANTS)
+    names = sys.argv[1:] or [n for n in VARIANTS if n != "stamps"]
     import shutil; shutil.rmtree(os.path.join(B.LIB_DIR, "variants"), ignore_errors=True)
     with ThreadPoolExecutor(4) as ex:
         for p in ex.map(lambda n: B.build_variant(n, VARIANTS[n]), names):

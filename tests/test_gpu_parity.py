@@ -148,6 +148,60 @@ def test_ragged_sizes_vs_oracle(N, closed):
     compare_outputs(mt, omt, True, f"N{N}.mt")
 
 
+def _segment_variants(seg, rng):
+    """Segment lists the entry-stream builder must handle: shuffled order (every
+    segment its own chain), reversed segments, split chains with duplicates and a
+    zero-length segment, and a ring with no segments."""
+    perm = seg[rng.permutation(len(seg))]
+    rev = seg.copy()
+    flip = rng.random(len(seg)) < 0.5
+    rev[flip] = rev[flip][:, [2, 3, 0, 1]]
+    cut = len(seg) // 3
+    split = np.vstack([seg[cut:], seg[:cut], seg[:2], seg[5:6, [0, 1, 0, 1]]])
+    return {"shuffled": perm, "reversed": rev, "split_dup_zero": split, "empty": seg[:0]}
+
+
+@pytest.mark.parametrize("closed", [True, False])
+def test_segment_lists_vs_oracle(closed):
+    """Corridor over arbitrary segment lists (rl_corridor.h entry streams) == oracle."""
+    _lib_or_skip()
+    rng = np.random.default_rng(11)
+    case = O.load_case("track_competition_map2")
+    base = O.case_problem(case)
+    cfg = O.case_cfg(case)
+    cfg.max_outer_iters = 4
+    for which in ("inner", "outer"):
+        for name, seg in _segment_variants(getattr(base, f"{which}_seg"), rng).items():
+            kw = dict(center=base.center, L=base.L, inner_seg=base.inner_seg, outer_seg=base.outer_seg,
+                      veh_width=base.veh_width, closed=closed)
+            kw[f"{which}_seg"] = seg
+            prob = abi.Problem(**kw)
+            mc, mt = raceline.optimize_batch(prob, cfg, [0, 4], 2)
+            omc, omt = O.run_oracle(prob, cfg, seeds=[0, 4], B=2)
+            compare_outputs(mc, omc, False, f"{which}.{name}.mc")
+            compare_outputs(mt, omt, True, f"{which}.{name}.mt")
+
+
+def test_dense_rings_vs_oracle():
+    """Rings of 1000+ segments (many 32-entry blocks), N=1500."""
+    _lib_or_skip()
+    N = 1500
+    t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+    center = np.stack([30 * np.cos(t) + 3 * np.cos(3 * t), 18 * np.sin(t)], axis=1)
+    k = np.linspace(0, 2 * np.pi, 1037, endpoint=False)
+    inner = np.stack([27 * np.cos(k) + 3 * np.cos(3 * k), 15.5 * np.sin(k)], axis=1)
+    outer = np.stack([33 * np.cos(k) + 3 * np.cos(3 * k), 20.5 * np.sin(k)], axis=1)
+    L = float(np.sum(np.hypot(*np.diff(np.vstack([center, center[:1]]), axis=0).T)))
+    prob = abi.Problem(center=center, L=L, inner_seg=raceline.ring_edges(inner),
+                       outer_seg=raceline.ring_edges(outer), veh_width=1.0, closed=True)
+    cfg = abi.default_cfg()
+    cfg.max_outer_iters = 4
+    mc, mt = raceline.optimize_batch(prob, cfg, [0, 1], 2)
+    omc, omt = O.run_oracle(prob, cfg, seeds=[0, 1], B=2)
+    compare_outputs(mc, omc, False, "dense.mc")
+    compare_outputs(mt, omt, True, "dense.mt")
+
+
 def test_plan_rerun_is_deterministic():
     _lib_or_skip()
     case = O.load_case("track_competition_map2")
