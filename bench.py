@@ -48,14 +48,13 @@ def load_problem(name: str):
 
 
 def flops_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: float = 0.0) -> float:
-    """Algorithmic fp64 flops per outer iteration: +,-,*,/,sqrt each 1.
-    per sample per evaluation 35 (min-curv) / 38 (min-time: γ² terms),
-    per sample per outer: lin-geom 40, update+normals 14, corridor 2·(Ei+Eo)·8 + (Ei or Eo)·14."""
-    per_eval = 38.0 if mintime else 35.0
-    fl = N * (per_eval * E_k + 40 + 14 + 16 * Eseg + 7 * Eseg)
-    if mintime:
-        fl += N * (30 + 2 * 25 * S + 20)   # κ, v-pass sweeps (fwd+bwd step ≈25 flops), γ²
-    return fl
+    """Algorithmic fp64 flops per outer iteration, SURVEY.md §8d's per-unit figure:
+    34 (min-curv) / 36 (min-time) per sample per evaluation, plus the corridor's
+    2·(Ei+Eo) ray tests per sample at 12 flops + 1 reciprocal each.  (The kernel
+    skips most ray tests exactly — rl_corridor.h — so it executes fewer; the
+    executed count from the PMC counters is reported beside it.)"""
+    per_eval = 36.0 if mintime else 34.0
+    return N * (per_eval * E_k + 2 * Eseg * 13)
 
 
 def bytes_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: float = 0.0) -> float:
@@ -65,15 +64,16 @@ def bytes_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: flo
     return N * (80 * E_k + 224) + 32 * Eseg
 
 
-def read_pmc_traffic(tag: str):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), or None."""
+def read_pmc(tag: str, key: str = "hbm_bytes_per_launch"):
+    """Per-launch figure (HBM bytes, executed fp64 flops) from the committed rocprofv3
+    PMC summary profiles/pmc_traffic.json (scripts/pmc.sh + pmc_summary.py), or None."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(tag, {}).get("hbm_bytes_per_launch")
+        return d.get(tag, {}).get(key)
     except Exception:
         return None
 
@@ -297,7 +297,7 @@ def main():
     achieved_tf = fl_launch / (k_ms * 1e-3) / 1e12
     roofline = {
         "bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 4), "traffic": read_pmc_traffic("c2_mincurv"),
+        "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 4), "traffic": read_pmc("c2_mincurv"),
         "kernel": "rl_optimize_kernel<8,256,closed,mincurv>", "kernel_ms": round(k_ms, 3),
         "note": "fp64 compute roof (VALU; MI355X fp64 vector = fp64 dense-matrix peak = 78.6 TF): "
                 "the instance state stays in VGPR/LDS, so HBM is not the binding roof",
@@ -305,6 +305,9 @@ def main():
         "streaming_model_frac_of_hbm": round(by_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
         "evals_per_outer": round(E_k, 2),
     }
+    fl_pmc = read_pmc("c2_mincurv", "fp64_flops_per_launch")
+    if fl_pmc:
+        roofline["executed_fp64_TFLOPs_pmc"] = round(fl_pmc / (k_ms * 1e-3) / 1e12, 3)
 
     extras = {}
     if not args.no_extras:

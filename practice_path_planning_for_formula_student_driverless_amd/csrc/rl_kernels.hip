@@ -36,7 +36,10 @@
 
 namespace rl {
 
-constexpr int CK = 4;   // corridor sub-chunk (samples per ray-scan pass)
+#ifndef RL_CK
+#define RL_CK 2
+#endif
+constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per ring pass)
 
 // Diagnostic build only (-DRL_STAMPS=1): per-phase s_memtime totals of each
 // workgroup's wave 0, written to a device array no other code reads.
@@ -148,11 +151,23 @@ struct alignas(16) Smem {
 #ifndef RL_MID_W
 #define RL_MID_W 2
 #endif
+// min-time at 1024 < N <= 2048: the extra γ² state favours 4 samples per lane
+#ifndef RL_MIDMT_K
+#define RL_MIDMT_K 4
+#endif
+#ifndef RL_MIDMT_T
+#define RL_MIDMT_T 512
+#endif
+#ifndef RL_MIDMT_W
+#define RL_MIDMT_W 2
+#endif
 
 // waves per SIMD to keep resident (caps the register budget the compiler may use)
 template <int K, int T>
 struct MinWaves {
-    static constexpr int value = (K == RL_MID_K && T == RL_MID_T) ? RL_MID_W : ((T >= 512) ? 1 : (T == 64 ? 4 : 2));
+    static constexpr int value = (K == RL_MID_K && T == RL_MID_T)       ? RL_MID_W
+                                 : (K == RL_MIDMT_K && T == RL_MIDMT_T) ? RL_MIDMT_W
+                                 : ((T >= 512) ? 1 : (T == 64 ? 4 : 2));
 };
 
 template <int K, int T, bool CLOSED, bool MT>
@@ -298,19 +313,20 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin), CK samples
     // at a time through the per-lane candidate scan of rl_corridor.h
     auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
+        constexpr int CKK = CK < K ? CK : K;
 #pragma unroll
-        for (int c = 0; c < K; c += CK) {
-            double qx[CK], qy[CK], ux[CK], uy[CK], lc[CK], hc[CK];
-            bool act[CK];
+        for (int c = 0; c < K; c += CKK) {
+            double qx[CKK], qy[CKK], ux[CKK], uy[CKK], lc[CKK], hc[CKK];
+            bool act[CKK];
 #pragma unroll
-            for (int k = 0; k < CK; ++k) {
+            for (int k = 0; k < CKK; ++k) {
                 const int i = own(c + k);
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                 act[k] = c + k < cnt;
             }
-            corridor_bounds<CK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lc, hc);
+            corridor_bounds<CKK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lc, hc);
 #pragma unroll
-            for (int k = 0; k < CK; ++k) {
+            for (int k = 0; k < CKK; ++k) {
                 hi[c + k] = act[k] ? hc[k] : 0.0;
                 lo[c + k] = act[k] ? lc[k] : 0.0;
             }
@@ -487,6 +503,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         double dl0, dr0;
         xpub(0, a, dl0, dr0);
         __syncthreads();
+#ifdef RL_EXP_BAR      // experiment: one extra barrier per evaluation (cost probe)
+        __syncthreads();
+#endif
         double lv, rv;
         xget(0, dl0, dr0, lv, rv);
         fill_pad(a, rv);
@@ -512,6 +531,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         xpub(3, a1v, dl3, dr3);
         pJ = wave_sum(pJ);
         pJsm = wave_sum(pJsm);
+#ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
+        {
+            double xx = wave_sum(pJ * 0.5);
+            asm volatile("" ::"v"(xx));
+        }
+#endif
         if (trial) pdec = wave_sum(pdec);
         if (lane == 0) { sm.red[0][wid] = pJ; sm.red[1][wid] = pJsm; sm.red[2][wid] = pdec; }
         __syncthreads();
@@ -782,13 +807,18 @@ static hipError_t launch_kt(const KParams& p, bool mt, hipStream_t st) {
     if (p.closed) return mt ? launch_t<K, T, true, true>(p, st) : launch_t<K, T, true, false>(p, st);
     return mt ? launch_t<K, T, false, true>(p, st) : launch_t<K, T, false, false>(p, st);
 }
+template <int K, int T, bool MT>
+static hipError_t launch_ktm(const KParams& p, hipStream_t st) {
+    return p.closed ? launch_t<K, T, true, MT>(p, st) : launch_t<K, T, false, MT>(p, st);
+}
 
 // variant table by N: (K samples per lane, T lanes per instance)
 //   N <= 256          (4, 64)      one wave per instance
 //   N <= 1024         (8, 128)
-//   N <= 2048         (RL_MID_K, RL_MID_T)   default (8, 256)
+//   N <= 2048         (RL_MID_K, RL_MID_T)   default (8, 256); min-time (RL_MIDMT_K, RL_MIDMT_T) = (4, 512)
 //   N <= 4096         (8, 512)
 static_assert(RL_MID_K * RL_MID_T == 2048, "mid variant must cover N <= 2048");
+static_assert(RL_MIDMT_K * RL_MIDMT_T == 2048, "mid min-time variant must cover N <= 2048");
 int pick_k(int N) {
     if (N <= 4 * 64) return 4;
     if (N <= 8 * 128) return 8;
@@ -801,7 +831,8 @@ hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
     if (p.N <= 4 * 64) return launch_kt<4, 64>(p, mintime, st);
     if (p.N <= 8 * 128) return launch_kt<8, 128>(p, mintime, st);
-    if (p.N <= 2048) return launch_kt<RL_MID_K, RL_MID_T>(p, mintime, st);
+    if (p.N <= 2048)
+        return mintime ? launch_ktm<RL_MIDMT_K, RL_MIDMT_T, true>(p, st) : launch_ktm<RL_MID_K, RL_MID_T, false>(p, st);
     return launch_kt<8, 512>(p, mintime, st);
 }
 
