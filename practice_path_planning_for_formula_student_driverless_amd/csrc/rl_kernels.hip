@@ -79,18 +79,16 @@ __device__ __forceinline__ double wave_sum(double x) {
     x += dpp<0x128>(x);   // row_ror:8
     return (readlane(x, 0) + readlane(x, 16)) + (readlane(x, 32) + readlane(x, 48));
 }
-// lane l <- lane l-1 (DPP wave_shr:1); lane 0 gets 0
-__device__ __forceinline__ double dpp_from_left(double x) {
-    int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xf, 0xf, false);
+// lane l <- lane l-1 (wave_shr:1); lane 0 keeps `edge` (bound_ctrl off: no write)
+__device__ __forceinline__ double dpp_from_left_or(double x, double edge) {
+    int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x138, 0xf, 0xf, false);
+    int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x138, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
-// lane l <- lane l+1 (DPP wave_shl:1); lane 63 gets 0
-__device__ __forceinline__ double dpp_from_right(double x) {
-    int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xf, 0xf, false);
+// lane l <- lane l+1 (wave_shl:1); lane 63 keeps `edge`
+__device__ __forceinline__ double dpp_from_right_or(double x, double edge) {
+    int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x130, 0xf, 0xf, false);
+    int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x130, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
 // keep v opaque to loop-invariant code motion (stops hoisting of per-sample addresses)
@@ -193,6 +191,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     // need no masking.
     const int wid_u = __builtin_amdgcn_readfirstlane(wid);
     const bool part_wave = (cntL != K) && (((Ta - 1) >> 6) == wid_u);
+    // wave-uniform: this wave holds the last active thread or lies beyond it
+    const bool tail_wave = wid_u >= ((Ta - 1) >> 6);
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
@@ -202,6 +202,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     const double two_h = 2 * h, hh = h * h;              // ref:602-603 divisors
     const double lam = C.lambda_smooth;
     const double lam2 = 2.0 * lam;                       // ref:673 2.0*lambda_smooth*gsm
+    // PGD constants in registers (the cfg lives in global memory the kernel also writes)
+    const double step_init = C.step_init, step_min = C.step_min, armijo_c = C.armijo_c;
+    const int max_inner = C.max_inner_iters;
 
     const size_t off = (size_t)b * (size_t)N;
     double* __restrict__ X = p.x + off;                  // P.x (state, then output)
@@ -212,11 +215,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     double* __restrict__ ALAST = p.alpha_last + off;
 
     // ---- neighbour exchange (DPP in-wave, LDS across waves and for the wrap) ----
-    // before a barrier: dl/dr receive the in-wave neighbour values
-    auto xpub = [&](int slot, const double (&a)[K], double& dl, double& dr) RL_AI {
+    // before a barrier: the wave's edge values (and the wrap value) go to LDS
+    auto xpub = [&](int slot, const double (&a)[K]) RL_AI {
         const double first = a[0], last = a[K - 1];
-        dl = dpp_from_left(last);
-        dr = dpp_from_right(first);
         *((lane == 0) ? &sm.eF[slot][wid] : &sm.sink[lane]) = first;
         *((lane == 63) ? &sm.eL[slot][wid] : &sm.sink[lane]) = last;
         if (cntL == K) {
@@ -226,15 +227,18 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             if (tid == Ta - 1) sm.wL[slot] = lv;
         }
     };
-    // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped)
-    auto xget = [&](int slot, double dl, double dr, double& lv, double& rv) RL_AI {
+    // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped).
+    // In-wave neighbours by DPP; lanes 0 / 63 keep the other wave's edge value.
+    auto xget = [&](int slot, const double (&a)[K], double& lv, double& rv) RL_AI {
         const double el = (wid > 0) ? sm.eL[slot][(wid > 0) ? wid - 1 : 0] : sm.wL[slot];   // wave-uniform reads
         const double ef = sm.eF[slot][(wid + 1 < NW) ? wid + 1 : 0];
-        const double e0 = sm.eF[slot][0];
-        lv = (lane == 0) ? el : dl;
-        rv = (lane == 63) ? ef : dr;
-        if (tid == Ta - 1) rv = e0;
-        if (!active) { lv = 0.0; rv = 0.0; }
+        lv = dpp_from_left_or(a[K - 1], el);
+        rv = dpp_from_right_or(a[0], ef);
+        if (tail_wave) {
+            const double e0 = sm.eF[slot][0];
+            if (tid == Ta - 1) rv = e0;
+            if (!active) { lv = 0.0; rv = 0.0; }
+        }
     };
     // the last active thread's padding slots take the right neighbour, so every
     // stencil reads a[k+1] (k<K-1) or rv (k=K-1) uniformly
@@ -482,7 +486,6 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     double G2[K];                                   // γ² (min-time)
     double lo[K], hi[K], al[K], gr[K], an[K];       // corridor, α, grad, α_trial
     double q1[K], q2[K], a1v[K];                    // gradient stencil inputs of the last evaluation
-    double dl1, dr1, dl2, dr2, dl3, dr3;            // in-wave neighbours of q1, q2, a1v
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
     // of the trial vector a: J (uniform across the workgroup) and the Armijo
@@ -500,16 +503,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 for (int k = 0; k < K; ++k) pdec += gr[k] * (a[k] - al[k]);
             }
         }
-        double dl0, dr0;
-        xpub(0, a, dl0, dr0);
+        xpub(0, a);
         __syncthreads();
 #ifdef RL_EXP_BAR      // experiment: one extra barrier per evaluation (cost probe)
         __syncthreads();
 #endif
         double lv, rv;
-        xget(0, dl0, dr0, lv, rv);
+        xget(0, a, lv, rv);
         fill_pad(a, rv);
         double pJ = 0.0, pJsm = 0.0;
+        double jz[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const double2 c01 = sm.u.coef[0][k][tid];   // (A1, A2)
@@ -519,16 +522,23 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             double x1 = d1_at(k, am, a[k], ap);
             double x2 = d2_at(k, am, a[k], ap);
             double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
-            double jz = MT ? (G2[k] * r * r) : (r * r);
+            jz[k] = MT ? (G2[k] * r * r) : (r * r);
             double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
             q1[k] = c01.x * Wz;
             q2[k] = c01.y * Wz;
             a1v[k] = x1;
-            if (!part_wave || k < cnt) { pJ += jz; pJsm += x1 * x1; }
         }
-        xpub(1, q1, dl1, dr1);
-        xpub(2, q2, dl2, dr2);
-        xpub(3, a1v, dl3, dr3);
+        if (part_wave) {            // wave-uniform: only the wave with the partial chunk masks
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k < cnt) { pJ += jz[k]; pJsm += a1v[k] * a1v[k]; }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) { pJ += jz[k]; pJsm += a1v[k] * a1v[k]; }
+        }
+        xpub(1, q1);
+        xpub(2, q2);
+        xpub(3, a1v);
         pJ = wave_sum(pJ);
         pJsm = wave_sum(pJsm);
 #ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
@@ -550,9 +560,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     // gradient of the last evaluation (ref:668-673 / 886-893)
     auto eval_grad = [&]() RL_AI {
         double l1, r1, l2, r2, l3, r3;
-        xget(1, dl1, dr1, l1, r1);
-        xget(2, dl2, dr2, l2, r2);
-        xget(3, dl3, dr3, l3, r3);
+        xget(1, q1, l1, r1);
+        xget(2, q2, l2, r2);
+        xget(3, a1v, l3, r3);
         fill_pad(q1, r1);
         fill_pad(q2, r2);
         fill_pad(a1v, r3);
@@ -648,10 +658,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
             if (outer == MO) {
                 // ax and lap time (ref:854-860)
-                double dl, dr, lv, rv;
-                xpub(0, v, dl, dr);
+                double lv, rv;
+                xpub(0, v);
                 __syncthreads();
-                xget(0, dl, dr, lv, rv);
+                xget(0, v, lv, rv);
                 double lt = 0.0;
                 if (active) {
 #pragma unroll
@@ -739,13 +749,13 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         }
         RL_STAMP(3);
         // PGD + Armijo (ref:723-742 / 996-1026)
-        double step = C.step_init;
+        double step = step_init;
         double dec;
         double J = eval_j(al, false, dec);
         eval_grad();
         int evals = 1, accepts = 0;
         double J_prev = J;
-        for (int it = 0; it < C.max_inner_iters; ++it) {
+        for (int it = 0; it < max_inner; ++it) {
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
@@ -758,7 +768,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 }
                 double Jn = eval_j(an, true, dec);
                 ++evals;
-                if (Jn <= J + C.armijo_c * dec) {
+                if (Jn <= J + armijo_c * dec) {
 #pragma unroll
                     for (int k = 0; k < K; ++k) al[k] = an[k];
                     eval_grad();
@@ -769,7 +779,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 }
                 step *= 0.5;
                 bt++;
-                if (step < C.step_min) break;
+                if (step < step_min) break;
             }
             if (!accepted) break;
             if (fabs(J_prev - J) < 1e-10) break;
