@@ -72,12 +72,21 @@ __device__ __forceinline__ double readlane(double x, int l) {
 // wave-uniform sum of x over the 64 lanes: DPP butterflies inside each 16-lane row
 // (quad_perm, row_ror:4, row_ror:8), then the four row sums via readlane, combined
 // in a fixed order.  No LDS round trip.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_rows(double x) {     // rows outside ROWS read 0
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWS, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROWS, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_sum(double x) {
     x += dpp<0xB1>(x);    // quad_perm [1,0,3,2]
     x += dpp<0x4E>(x);    // quad_perm [2,3,0,1]
     x += dpp<0x124>(x);   // row_ror:4
-    x += dpp<0x128>(x);   // row_ror:8
-    return (readlane(x, 0) + readlane(x, 16)) + (readlane(x, 32) + readlane(x, 48));
+    x += dpp<0x128>(x);   // row_ror:8  -> every lane holds its row sum r0..r3
+    x += dpp_rows<0x142, 0xa>(x);   // row_bcast:15 into rows 1,3: r0+r1, r2+r3
+    x += dpp_rows<0x143, 0xc>(x);   // row_bcast:31 into rows 2,3: lane 63 = (r2+r3)+(r0+r1)
+    return readlane(x, 63);
 }
 // lane l <- lane l-1 (wave_shr:1); lane 0 keeps `edge` (bound_ctrl off: no write)
 __device__ __forceinline__ double dpp_from_left_or(double x, double edge) {
@@ -492,15 +501,18 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     // decrease Σ grad*(a-α) (ref:733 / 1009); q1,q2,D1α and their in-wave
     // neighbours are left for eval_grad.
     auto eval_j = [&](double (&a)[K], bool trial, double& dec) RL_AI -> double {
+        // J and the Armijo decrease only steer accept/stop decisions; the α iterates
+        // never read them, so their accumulations use fma (their summation order
+        // already differs from the reference's serial loop, ref:661-666)
         double pdec = 0.0;
         if (trial) {
             if (part_wave) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (k < cnt) pdec += gr[k] * (a[k] - al[k]);
+                    if (k < cnt) pdec = __builtin_fma(gr[k], a[k] - al[k], pdec);
             } else {
 #pragma unroll
-                for (int k = 0; k < K; ++k) pdec += gr[k] * (a[k] - al[k]);
+                for (int k = 0; k < K; ++k) pdec = __builtin_fma(gr[k], a[k] - al[k], pdec);
             }
         }
         xpub(0, a);
@@ -512,7 +524,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         xget(0, a, lv, rv);
         fill_pad(a, rv);
         double pJ = 0.0, pJsm = 0.0;
-        double jz[K];
+        double jr[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const double2 c01 = sm.u.coef[0][k][tid];   // (A1, A2)
@@ -522,25 +534,29 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             double x1 = d1_at(k, am, a[k], ap);
             double x2 = d2_at(k, am, a[k], ap);
             double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
-            jz[k] = MT ? (G2[k] * r * r) : (r * r);
+            jr[k] = r;
             double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
             q1[k] = c01.x * Wz;
             q2[k] = c01.y * Wz;
             a1v[k] = x1;
         }
+        auto acc = [&](int k) RL_AI {    // Σ γ²r² (ref:881) / Σ z² (ref:661), Σ a1² (ref:662 / 882)
+            pJ = __builtin_fma(MT ? G2[k] * jr[k] : jr[k], jr[k], pJ);
+            pJsm = __builtin_fma(a1v[k], a1v[k], pJsm);
+        };
         if (part_wave) {            // wave-uniform: only the wave with the partial chunk masks
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (k < cnt) { pJ += jz[k]; pJsm += a1v[k] * a1v[k]; }
+                if (k < cnt) acc(k);
         } else {
 #pragma unroll
-            for (int k = 0; k < K; ++k) { pJ += jz[k]; pJsm += a1v[k] * a1v[k]; }
+            for (int k = 0; k < K; ++k) acc(k);
         }
+        pJ = __builtin_fma(lam, pJsm, pJ);             // J += λ·Jsm (ref:663 / 883), per lane
         xpub(1, q1);
         xpub(2, q2);
         xpub(3, a1v);
         pJ = wave_sum(pJ);
-        pJsm = wave_sum(pJsm);
 #ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
         {
             double xx = wave_sum(pJ * 0.5);
@@ -548,12 +564,11 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         }
 #endif
         if (trial) pdec = wave_sum(pdec);
-        if (lane == 0) { sm.red[0][wid] = pJ; sm.red[1][wid] = pJsm; sm.red[2][wid] = pdec; }
+        if (lane == 0) { sm.red[0][wid] = pJ; sm.red[2][wid] = pdec; }
         __syncthreads();
-        double J = sm.red[0][0], Jsm = sm.red[1][0], D = sm.red[2][0];
+        double J = sm.red[0][0], D = sm.red[2][0];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) { J += sm.red[0][w]; Jsm += sm.red[1][w]; D += sm.red[2][w]; }
-        J += lam * Jsm;                                 // ref:666 / 883
+        for (int w = 1; w < NW; ++w) { J += sm.red[0][w]; D += sm.red[2][w]; }
         dec = D;
         return J;
     };
