@@ -88,17 +88,16 @@ __device__ __forceinline__ bool next_bits(uint32_t (&w)[CK], bool (&h)[CK], int 
     return __any(any);
 }
 
-// one ring: ray distances along +n / -n with the safe_ray fallback applied
-// (ref:694-699), i.e. sp = safe(+n), sn = safe(-n), both >= 0
+// one ring's rays: nearest hit along +n (bp) and -n (bn), +inf if none, and ub2 >= the
+// squared point-to-segment minimum (from the walked candidates' endpoints; +inf if none)
 template <int CK>
-__device__ __forceinline__ void ring_scan(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
+__device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
                                           const double (&ux)[CK], const double (&uy)[CK], const bool (&act)[CK],
-                                          double (&sp)[CK], double (&sn)[CK]) {
+                                          double (&bp)[CK], double (&bn)[CK], double (&ub2)[CK]) {
     cdbl* V = as_cdbl(R.vtx);              // [M][2]
-    cdbl* SR = as_cdbl(R.rec);             // [M][8] SegRec fields (uniform reads)
     cu32* F = as_cu32(R.flag);
     const SegRec* __restrict__ S = R.rec;  // per-lane (divergent) reads
-    double dl[CK], g[CK], bp[CK], bn[CK], ub2[CK];
+    double dl[CK], g[CK];
     uint64_t pp[CK], pn[CK];       // side masks of the previous entry (wave lane masks, SGPR)
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
@@ -150,91 +149,127 @@ __device__ __forceinline__ void ring_scan(const RingDesc& R, const double (&qx)[
             }
         }
     }
-    // minDistanceToSegments_global only where a ray of this ring missed (safe_ray ref:696)
-    double md[CK];
-    bool need[CK];
-    bool any_need = false, any_ub = false;
+}
+
+// minDistanceToSegments_global (ref:501-512) for the samples with need[k], exact for
+// every sample whose minimum is <= rad[k] (md[k] = +inf or a value > rad[k] otherwise).
+// One lane-level filter per entry: the samples' bounding circle (centre q0, radius
+// max_k rad[k] + |q_k - q0|_1) against |mid - q0| <= R + half_len.
+template <int CK>
+__device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
+                                             const bool (&need)[CK], const double (&rad)[CK], double (&md)[CK]) {
+    cdbl* SR = as_cdbl(R.rec);             // [M][8] SegRec fields (uniform reads)
+    cu32* F = as_cu32(R.flag);
+    const SegRec* __restrict__ S = R.rec;
+    const double cx = qx[0], cy = qy[0];
+    double Rl = -1.0;
+    bool lneed = false;
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
         md[k] = INFINITY;
-        need[k] = act[k] && (!isfinite(bp[k]) || !isfinite(bn[k]));
-        any_need |= need[k];
-        any_ub |= need[k] && !isfinite(ub2[k]);
+        if (need[k]) Rl = fmax(Rl, rad[k] + (fabs(qx[k] - cx) + fabs(qy[k] - cy)) * (1.0 + 1e-12));
+        lneed |= need[k];
     }
-    if (__any(any_need)) {
-        if (__any(any_ub)) {          // no candidate at all: bound from every vertex
-            for (int v = 0; v < R.M; ++v) {
-                const double vx = V[2 * v], vy = V[2 * v + 1];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    const double dx = qx[k] - vx, dy = qy[k] - vy;
-                    ub2[k] = fmin(ub2[k], dx * dx + dy * dy);     // NaN padding is ignored
-                }
-            }
-        }
-        double lim[CK];
-#pragma unroll
-        for (int k = 0; k < CK; ++k) lim[k] = sqrt(ub2[k]) * (1.0 + 1e-9) + 1e-12;
-        for (int b0 = 0; b0 < R.M; b0 += 32) {
-            uint32_t w[CK];
-#pragma unroll
-            for (int k = 0; k < CK; ++k) w[k] = 0u;
+    for (int b0 = 0; b0 < R.M; b0 += 32) {
+        uint32_t w = 0u;
 #pragma unroll 8
-            for (int j = 0; j < 32; ++j) {
-                cdbl* sr = SR + 8 * (b0 + j);
-                const double mx = sr[5], my = sr[6], hr = sr[7];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    const double dx = qx[k] - mx, dy = qy[k] - my, r = lim[k] + hr;
-                    const bool skip = dx * dx + dy * dy > r * r;
-                    w[k] = (w[k] << 1) | (uint32_t)!skip;
-                }
-            }
-            const uint32_t f = F[b0 >> 5];
-#pragma unroll
-            for (int k = 0; k < CK; ++k) w[k] = need[k] ? (w[k] & f) : 0u;
-            bool h[CK];
-            int j[CK];
-            while (next_bits<CK>(w, h, j)) {
-                double x0[CK], y0[CK], sx[CK], sy[CK], dn[CK];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    const SegRec* s = S + b0 + j[k];
-                    x0[k] = s->x0; y0[k] = s->y0; sx[k] = s->vx; sy[k] = s->vy; dn[k] = s->denom;
-                }
-#pragma unroll
-                for (int k = 0; k < CK; ++k)
-                    if (h[k]) md[k] = smin(md[k], seg_dist_exact(x0[k], y0[k], sx[k], sy[k], dn[k], qx[k], qy[k]));
-            }
+        for (int j = 0; j < 32; ++j) {
+            cdbl* sr = SR + 8 * (b0 + j);
+            const double mx = sr[5], my = sr[6], hr = sr[7];
+            const double dx = cx - mx, dy = cy - my, r = Rl + hr;
+            const bool skip = dx * dx + dy * dy > r * r;
+            w = (w << 1) | (uint32_t)!skip;
         }
-    }
+        w = lneed ? (w & F[b0 >> 5]) : 0u;
+        while (__any(w != 0u)) {
+            const bool h = w != 0u;
+            const int j = h ? __clz(w) : 0;
+            w &= ~(0x80000000u >> j);
+            const SegRec* s = S + b0 + j;
+            const double x0 = s->x0, y0 = s->y0, sx = s->vx, sy = s->vy, dn = s->denom;
 #pragma unroll
-    for (int k = 0; k < CK; ++k) {
-        double a = bp[k], b = bn[k];
-        if (!isfinite(a)) a = md[k];
-        if (!isfinite(a)) a = 0.0;
-        if (!isfinite(b)) b = md[k];
-        if (!isfinite(b)) b = 0.0;
-        sp[k] = smax(0.0, a);
-        sn[k] = smax(0.0, b);
+            for (int k = 0; k < CK; ++k)
+                if (h && need[k]) md[k] = smin(md[k], seg_dist_exact(x0, y0, sx, sy, dn, qx[k], qy[k]));
+        }
     }
 }
 
-// corridor bounds for CK samples (ref:702-711); guard = width*0.5 + margin.
-// Inactive samples (act false: padding of a ragged chunk) do no exact work; their
-// outputs are meaningless and the caller zeroes them.
+// squared distance upper bound from every vertex of the ring (NaN padding ignored)
+template <int CK>
+__device__ __forceinline__ void ring_vertex_ub(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
+                                               double (&ub2)[CK]) {
+    cdbl* V = as_cdbl(R.vtx);
+    for (int v = 0; v < R.M; ++v) {
+        const double vx = V[2 * v], vy = V[2 * v + 1];
+#pragma unroll
+        for (int k = 0; k < CK; ++k) {
+            const double dx = qx[k] - vx, dy = qy[k] - vy;
+            ub2[k] = fmin(ub2[k], dx * dx + dy * dy);
+        }
+    }
+}
+
+// corridor bounds for CK samples (ref:694-711); guard = width*0.5 + margin.
+// dpos = min(safe(+n, inner), safe(+n, outer)), dneg likewise, where
+// safe(t, md) = max(0, t finite ? t : (md finite ? md : 0)) (ref:694-699).
+// A ring's fallback minimum md_r only enters through min(., other ring's value):
+// when the other ring's ray in that direction hit at s, any md_r >= s yields s
+// (std::min returns the same value on ties), so md_r is searched only within
+// rad = min(ub, s_max) and reported as +inf when it exceeds it.
+// Inactive samples (act false) do no exact work; the caller zeroes their outputs.
 template <int CK>
 __device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDesc& Ro, const double (&qx)[CK],
                                                 const double (&qy)[CK], const double (&ux)[CK],
                                                 const double (&uy)[CK], const bool (&act)[CK], double guard,
                                                 double (&lo)[CK], double (&hi)[CK]) {
-    double spi[CK], sni[CK], spo[CK], sno[CK];
-    ring_scan<CK>(Ri, qx, qy, ux, uy, act, spi, sni);
-    ring_scan<CK>(Ro, qx, qy, ux, uy, act, spo, sno);
+    double bp[2][CK], bn[2][CK], ub2[2][CK];
+    ring_rays<CK>(Ri, qx, qy, ux, uy, act, bp[0], bn[0], ub2[0]);
+    ring_rays<CK>(Ro, qx, qy, ux, uy, act, bp[1], bn[1], ub2[1]);
+    double md[2][CK];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const RingDesc& R = r == 0 ? Ri : Ro;
+        const int o = 1 - r;
+        bool need[CK], any_need = false, any_ub = false;
+        double rad[CK];
+#pragma unroll
+        for (int k = 0; k < CK; ++k) {
+            const bool mp = !isfinite(bp[r][k]), mn = !isfinite(bn[r][k]);
+            need[k] = act[k] && (mp || mn);
+            // largest value md_r can take and still matter (+inf: the other ring missed too)
+            double tau = -INFINITY;
+            if (mp) tau = fmax(tau, isfinite(bp[o][k]) ? smax(0.0, bp[o][k]) : INFINITY);
+            if (mn) tau = fmax(tau, isfinite(bn[o][k]) ? smax(0.0, bn[o][k]) : INFINITY);
+            rad[k] = tau;
+            any_need |= need[k];
+            any_ub |= need[k] && !isfinite(ub2[r][k]) && !isfinite(tau);
+        }
+        if (!__any(any_need)) {
+#pragma unroll
+            for (int k = 0; k < CK; ++k) md[r][k] = INFINITY;
+            continue;
+        }
+        if (__any(any_ub)) ring_vertex_ub<CK>(R, qx, qy, ub2[r]);   // no candidate at all (rare)
+#pragma unroll
+        for (int k = 0; k < CK; ++k) {
+            const double lim = sqrt(ub2[r][k]) * (1.0 + 1e-9) + 1e-12;   // >= the true minimum
+            rad[k] = fmin(lim, rad[k] * (1.0 + 1e-9) + 1e-12);
+        }
+        ring_mindist<CK>(R, qx, qy, need, rad, md[r]);
+    }
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
-        double dpos = smin(spi[k], spo[k]);
-        double dneg = smin(sni[k], sno[k]);
+        double s[2][2];            // [ring][+n, -n]
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int E = r == 0 ? Ri.E : Ro.E;
+            // md = +inf from a non-empty ring means "beyond the other ring's value"
+            const double mdv = isfinite(md[r][k]) ? smax(0.0, md[r][k]) : (E == 0 ? 0.0 : INFINITY);
+            s[r][0] = isfinite(bp[r][k]) ? smax(0.0, bp[r][k]) : mdv;
+            s[r][1] = isfinite(bn[r][k]) ? smax(0.0, bn[r][k]) : mdv;
+        }
+        double dpos = smin(s[0][0], s[1][0]);
+        double dneg = smin(s[0][1], s[1][1]);
         double hk = smax(0.0, dpos - guard);
         double lk = -smax(0.0, dneg - guard);
         if (!isfinite(hk)) hk = 0.0;

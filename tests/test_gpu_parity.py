@@ -182,6 +182,33 @@ def test_segment_lists_vs_oracle(closed):
             compare_outputs(mt, omt, True, f"{which}.{name}.mt")
 
 
+@pytest.mark.parametrize("radius,width", [(18.25, 4.0), (21.75, 4.0), (20.0, 1.4), (19.0, 2.2)])
+def test_offset_centerlines_vs_oracle(radius, width):
+    """Centerline hugging the inner ring, hugging the outer ring, and narrow tracks:
+    the point-to-ring fallback minimum lands on both sides of the other ring's ray
+    distance (rl_corridor.h radius tightening)."""
+    _lib_or_skip()
+    N = 700
+    t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+    wob = 1 + 0.04 * np.sin(5 * t)
+    center = np.stack([1.4 * radius * wob * np.cos(t), radius * wob * np.sin(t)], axis=1)
+    k = np.linspace(0, 2 * np.pi, 97, endpoint=False)
+    wk = 1 + 0.04 * np.sin(5 * k)
+    ri, ro = 20.0 - width / 2, 20.0 + width / 2
+    inner = np.stack([1.4 * ri * wk * np.cos(k), ri * wk * np.sin(k)], axis=1)
+    outer = np.stack([1.4 * ro * wk * np.cos(k), ro * wk * np.sin(k)], axis=1)
+    L = float(np.sum(np.hypot(*np.diff(np.vstack([center, center[:1]]), axis=0).T)))
+    cfg = abi.default_cfg()
+    cfg.max_outer_iters = 5
+    for closed in (True, False):
+        prob = abi.Problem(center=center, L=L, inner_seg=raceline.edges_for(inner, closed),
+                           outer_seg=raceline.edges_for(outer, closed), veh_width=0.6, closed=closed)
+        mc, mt = raceline.optimize_batch(prob, cfg, [0, 2, 9], 3)
+        omc, omt = O.run_oracle(prob, cfg, seeds=[0, 2, 9], B=3)
+        compare_outputs(mc, omc, False, f"off{radius}/{width}/{closed}.mc")
+        compare_outputs(mt, omt, True, f"off{radius}/{width}/{closed}.mt")
+
+
 def test_dense_rings_vs_oracle():
     """Rings of 1000+ segments (many 32-entry blocks), N=1500."""
     _lib_or_skip()
