@@ -39,6 +39,9 @@ namespace rl {
 #ifndef RL_CK
 #define RL_CK 2
 #endif
+#ifndef RL_SPEC_GRAD
+#define RL_SPEC_GRAD 0   // 1: interior of the next gradient ahead of the reduction (A/B: slower)
+#endif
 constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per ring pass)
 
 // Diagnostic build only (-DRL_STAMPS=1): per-phase s_memtime totals of each
@@ -491,9 +494,19 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         return acc;
     };
 
+    // gradient at own sample k from the stencil inputs around it (ref:668-673 / 886-893)
+    auto grad_at = [&](int k, double q1m, double q10, double q1p, double q2m, double q20, double q2p, double am,
+                       double a0, double ap) RL_AI -> double {
+        double g1 = d1t_at(k, q1m, q10, q1p);
+        double g2 = d2t_at(k, q2m, q20, q2p);
+        double gsm = d1t_at(k, am, a0, ap);
+        return 2.0 * (g1 + g2) + lam2 * gsm;
+    };
+
     // ---- state ------------------------------------------------------------
     double G2[K];                                   // γ² (min-time)
     double lo[K], hi[K], al[K], gr[K], an[K];       // corridor, α, grad, α_trial
+    double gn[K];                                   // next gradient, interior samples (speculative)
     double q1[K], q2[K], a1v[K];                    // gradient stencil inputs of the last evaluation
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
@@ -556,6 +569,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         xpub(1, q1);
         xpub(2, q2);
         xpub(3, a1v);
+#if RL_SPEC_GRAD
+        // the interior of the next gradient needs no neighbour: compute it now, ahead
+        // of the reduction (used only if the step is accepted)
+        if (!part_wave) {
+#pragma unroll
+            for (int k = 1; k + 1 < K; ++k)
+                gn[k] = grad_at(k, q1[k - 1], q1[k], q1[k + 1], q2[k - 1], q2[k], q2[k + 1], a1v[k - 1], a1v[k],
+                                a1v[k + 1]);
+        }
+#endif
         pJ = wave_sum(pJ);
 #ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
         {
@@ -578,16 +601,28 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         xget(1, q1, l1, r1);
         xget(2, q2, l2, r2);
         xget(3, a1v, l3, r3);
-        fill_pad(q1, r1);
-        fill_pad(q2, r2);
-        fill_pad(a1v, r3);
+        auto full = [&]() RL_AI {
+            fill_pad(q1, r1);
+            fill_pad(q2, r2);
+            fill_pad(a1v, r3);
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            double g1 = d1t_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1);
-            double g2 = d2t_at(k, (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2);
-            double gsm = d1t_at(k, (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
-            gr[k] = 2.0 * (g1 + g2) + lam2 * gsm;
+            for (int k = 0; k < K; ++k)
+                gr[k] = grad_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
+                                (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
+                                (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
+        };
+#if RL_SPEC_GRAD
+        if (part_wave) {
+            full();
+        } else {
+            gr[0] = grad_at(0, l1, q1[0], q1[1], l2, q2[0], q2[1], l3, a1v[0], a1v[1]);
+#pragma unroll
+            for (int k = 1; k + 1 < K; ++k) gr[k] = gn[k];
+            gr[K - 1] = grad_at(K - 1, q1[K - 2], q1[K - 1], r1, q2[K - 2], q2[K - 1], r2, a1v[K - 2], a1v[K - 1], r3);
         }
+#else
+        full();
+#endif
     };
 
     // ======================================================================
@@ -635,6 +670,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             __syncthreads();
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
             corridor(guard, lo, hi);
+#ifdef RL_EXP_CORR2    // experiment: the corridor twice (cost probe; same results)
+            corridor(guard, lo, hi);
+#endif
             if (outer == 0 && seed != 0) {                      // ref:720 + seed
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -777,9 +815,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     double ai = al[k] - step * gr[k];
-                    // min(hi, max(lo, ai)) (ref:731) with v_min/v_max_f64: same value
-                    // as the std:: forms incl. NaN handling (only the sign of a zero may differ)
-                    an[k] = fmin(hi[k], fmax(lo[k], ai));
+                    // std::min(hi, std::max(lo, ai)) (ref:731) as selects: v_min/v_max_f64
+                    // would return the other zero when lo = -0 / hi = +0 meet a zero, and
+                    // alpha_last is printed with its sign (ref:1372)
+                    an[k] = smin(hi[k], smax(lo[k], ai));
                 }
                 double Jn = eval_j(an, true, dec);
                 ++evals;

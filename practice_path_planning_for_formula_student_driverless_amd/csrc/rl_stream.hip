@@ -424,7 +424,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
-                for (int i = tid; i < N; i += TS) an_p[i] = fmin(HI[i], fmax(LO[i], al_p[i] - step * GR[i]));
+                for (int i = tid; i < N; i += TS) an_p[i] = smin(HI[i], smax(LO[i], al_p[i] - step * GR[i]));   // std:: semantics (ref:731)
                 __syncthreads();
                 const double Jn = eval_j(an_p, true, dec);
                 ++evals;

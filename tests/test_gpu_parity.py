@@ -32,9 +32,21 @@ def col_close(got, ref, what):
     return err
 
 
+def zero_signs_equal(got, ref, what):
+    """Exact zeros must carry the oracle's sign: the reference prints its columns
+    with operator<< (ref:1372, 1427), where -0.0 reads "-0"."""
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    z = ref == 0.0
+    bad = np.flatnonzero(z & (np.signbit(got) != np.signbit(ref)))
+    assert bad.size == 0, f"{what}: {bad.size} zeros with the wrong sign (first at {bad[:5]})"
+
+
 def compare_outputs(got: abi.Outputs, ref: abi.Outputs, mintime: bool, label: str, counters=True):
     for f in abi.OUT_F64 + (("v", "ax") if mintime else ()):
         col_close(getattr(got, f), getattr(ref, f), f"{label}.{f}")
+    for f in abi.OUT_F64 + (("v", "ax") if mintime else ()):
+        zero_signs_equal(getattr(got, f), getattr(ref, f), f"{label}.{f}")
     if mintime:
         rel = np.max(np.abs(got.lap - ref.lap) / np.abs(ref.lap))
         assert rel <= REL, f"{label}.lap rel {rel:.3e}"
@@ -64,6 +76,7 @@ def test_golden_case_vs_reference(name):
             continue
         for f in flds:
             col_close(getattr(got, f)[0], case[f"{pre}_{f}"], f"{name}.{pre}_{f}")
+            zero_signs_equal(getattr(got, f)[0], case[f"{pre}_{f}"], f"{name}.{pre}_{f}")
         if pre == "mt":
             assert abs(got.lap[0] - float(case["mt_lap"])) / float(case["mt_lap"]) <= REL
         np.testing.assert_array_equal(got.evals, orc.evals, err_msg=f"{name}.{pre}.evals")
