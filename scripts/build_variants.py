@@ -10,6 +10,7 @@ VARIANTS = {
     "k4t512w4": {"RL_MID_K": 4, "RL_MID_T": 512, "RL_MID_W": 4},
     "ck4": {"RL_CK": 4},
     "mt_k8t256": {"RL_MIDMT_K": 8, "RL_MIDMT_T": 256},
+    "exp_corr2": {"RL_EXP_CORR2": 1},
     "exp_bar": {"RL_EXP_BAR": 1},
     "exp_red": {"RL_EXP_RED": 1},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
