@@ -203,6 +203,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal on a one-GPU box only: every rank on cuda:0, gloo instead of RCCL
+    if os.environ.get("RL_BENCH_SAME_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("RL_BENCH_BACKEND", "nccl")
     import torch
 
     dist = None
@@ -210,7 +214,10 @@ def main():
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -233,11 +240,22 @@ def main():
 
     stream = torch.cuda.Stream(device=dev)
 
+    def summarize():
+        # per-instance summaries [B, 3]: Σ evaluations, Σ x, Σ α_last (SURVEY §8e's
+        # "gather of per-instance summaries, then selective fetches"); the full SoA
+        # results stay resident on each rank
+        return torch.stack([res["evals"].sum(1, dtype=torch.float64), res["x"].sum(1),
+                            res["alpha_last"].sum(1)], dim=1)
+
+    gathered = {}
+
     def step():
         plan.run(stream.cuda_stream)
         if world > 1:
             with torch.cuda.stream(stream):
-                D.gather_to_root(res, world, rank)     # RCCL gather over xGMI (only collective)
+                out = D.gather_to_root({"summary": summarize()}, world, rank)   # RCCL over xGMI
+                if rank == 0:
+                    gathered["summary"] = out["summary"]
 
     for _ in range(args.warmup):
         step()
@@ -276,6 +294,13 @@ def main():
         return
 
     # ---- parity of this run (outside the timed region) ----
+    summary_check = None
+    if world > 1:
+        allsum = torch.cat(gathered["summary"]).cpu().numpy()          # [world*B, 3], rank-major
+        mine = summarize().cpu().numpy()
+        summary_check = {"instances_gathered": int(allsum.shape[0]),
+                         "rank0_rows_equal": bool(np.array_equal(allsum[:B], mine)),
+                         "seed0_x_sum_vs_reference": float(abs(allsum[0, 1] - float(np.sum(case["mc_x"]))))}
     evals = res["evals"].cpu().numpy()
     E_k = float(evals.mean())
     x0 = res["x"][0].cpu().numpy()
@@ -357,11 +382,12 @@ def main():
         "data": "competition_map1 cones from the reference repo -> reference steps 1-6 (fixture); synthetic alpha-seeds",
         "config": {"workload": "C2: competition_map1 closed, N=2000, B=1024 alpha-seeds per GPU, min-curvature, "
                                "14 outer iterations, default cfg::Config", "N": N, "batch_per_gpu": B,
-                   "global_batch": world * B, "parallelism": f"instances sharded over {world} GPU(s), RCCL gather"},
+                   "global_batch": world * B, "parallelism": f"dp{world}: instances sharded over {world} GPU(s); per-step RCCL gather of "
+                                  f"per-instance summaries to rank 0"},
         "tracks_per_s": round(tracks_per_s, 2),
         "roofline": roofline,
         "cpu_baseline": cpu,
-        "parity": parity,
+        "parity": parity if summary_check is None else {**parity, "gather": summary_check},
         **extras,
     }
     print(json.dumps(out), flush=True)

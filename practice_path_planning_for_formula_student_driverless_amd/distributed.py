@@ -33,7 +33,10 @@ def gather_to_root(tensors: Dict[str, "object"], world: int, rank: int, group=No
     import torch.distributed as dist
 
     out = {} if rank == 0 else None
+    host = dist.get_backend(group) == "gloo"      # gloo gathers host tensors (CPU tests, rehearsal)
     for name, t in tensors.items():
+        if host and t.is_cuda:
+            t = t.cpu()
         lst = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
         dist.gather(t, lst, dst=0, group=group)
         if rank == 0:
