@@ -39,6 +39,9 @@ namespace rl {
 #ifndef RL_CK
 #define RL_CK 2
 #endif
+#ifndef RL_MFMA_RED
+#define RL_MFMA_RED 0    // 1: evaluation sums on the fp64 matrix core (A/B: slower)
+#endif
 #ifndef RL_SPEC_GRAD
 #define RL_SPEC_GRAD 0   // 1: interior of the next gradient ahead of the reduction (A/B: slower)
 #endif
@@ -90,6 +93,18 @@ __device__ __forceinline__ double wave_sum(double x) {
     x += dpp_rows<0x142, 0xa>(x);   // row_bcast:15 into rows 1,3: r0+r1, r2+r3
     x += dpp_rows<0x143, 0xc>(x);   // row_bcast:31 into rows 2,3: lane 63 = (r2+r3)+(r0+r1)
     return readlane(x, 63);
+}
+// wave-uniform sum of x on the fp64 matrix core: with B = ones, v_mfma_f64_16x16x4
+// gives each lane the four row sums S_{4g..4g+3} of its 16-lane group g (S_i = Σ_k
+// x_{i+16k}); their sum T_g fed through a second MFMA leaves T_0+T_1+T_2+T_3 in every
+// lane.  Two MFMAs and three VALU adds instead of ~20 VALU (DPP movs, adds, readlanes).
+typedef double rl_v4d __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double wave_sum_mfma(double x) {
+    const rl_v4d z = {0.0, 0.0, 0.0, 0.0};
+    const rl_v4d d = __builtin_amdgcn_mfma_f64_16x16x4f64(x, 1.0, z, 0, 0, 0);
+    const double t = (d[0] + d[1]) + (d[2] + d[3]);
+    const rl_v4d e = __builtin_amdgcn_mfma_f64_16x16x4f64(t, 1.0, z, 0, 0, 0);
+    return e[0];
 }
 // lane l <- lane l-1 (wave_shr:1); lane 0 keeps `edge` (bound_ctrl off: no write)
 __device__ __forceinline__ double dpp_from_left_or(double x, double edge) {
@@ -579,14 +594,22 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                                 a1v[k + 1]);
         }
 #endif
+#if RL_MFMA_RED
+        pJ = wave_sum_mfma(pJ);
+#else
         pJ = wave_sum(pJ);
+#endif
 #ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
         {
             double xx = wave_sum(pJ * 0.5);
             asm volatile("" ::"v"(xx));
         }
 #endif
+#if RL_MFMA_RED
+        if (trial) pdec = wave_sum_mfma(pdec);
+#else
         if (trial) pdec = wave_sum(pdec);
+#endif
         if (lane == 0) { sm.red[0][wid] = pJ; sm.red[2][wid] = pdec; }
         __syncthreads();
         double J = sm.red[0][0], D = sm.red[2][0];
