@@ -190,6 +190,32 @@ def run_c5(world, rank, local, dev, dist):
             "seed0_vs_reference_max_rel_err": rel}
 
 
+def run_step6(world, rank):
+    """step 6 (compute_geom_and_save) for competition_map1 at
+    samples=2000 on the GPU (rl_geom) vs the CPU oracle on the same inputs; the rows
+    formatted as <base>_with_geom.csv are compared with the reference's own file."""
+    import oracle_lib as O
+
+    if rank != 0:
+        return None
+    case = O.load_geom_case("cmap1_n2000")
+    gp, cfg = O.geom_problem(case), O.geom_cfg(case)
+    raceline.compute_geom(gp, cfg)                       # warm-up (module load, first launch)
+    walls, kms = [], []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        rows, kms_i = raceline.compute_geom(gp, cfg, return_ms=True)
+        walls.append(time.perf_counter() - t0)
+        kms.append(kms_i)
+    t0 = time.perf_counter()
+    O.run_oracle_geom(gp, cfg)
+    cpu_s = time.perf_counter() - t0
+    return {"rows": int(rows.shape[0]), "segments": int(gp.inner_seg.shape[0] + gp.outer_seg.shape[0]),
+            "kernel_ms": round(float(np.median(kms)), 4), "wall_ms_incl_transfers": round(1e3 * float(np.median(walls)), 3),
+            "cpu_oracle_ms_1core": round(1e3 * cpu_s, 3),
+            "csv_bytes_equal_reference": raceline.format_geom_csv(rows).encode() == case["_csv"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -285,6 +311,7 @@ def main():
     tracks_per_s = world * B * args.steps / elapsed
 
     c4 = None if args.no_extras else run_c4(world, rank, local, dev, dist)
+    st6 = None if args.no_extras else run_step6(world, rank)
     c5 = None if args.no_extras else run_c5(world, rank, local, dev, dist)
     if rank != 0:
         plan.close()
@@ -363,6 +390,8 @@ def main():
         extras["c4_sweep_7tracks_x_512"] = c4
     if c5 is not None:
         extras["c5_oval_n10000"] = c5
+    if st6 is not None:
+        extras["step6_geom_cmap1_n2000"] = st6
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(prob, cfg)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 1
+#define RL_ABI_VERSION 2
 
 /* error codes */
 #define RL_OK          0
@@ -180,10 +180,47 @@ int rl_plan_device_outputs(rl_plan* plan, int32_t which, rl_out* dev_out);
  * result storage of mode `which`; NULL fields keep the plan's own buffers.  Lets a
  * framework (e.g. torch tensors for an RCCL gather) receive results without copies. */
 int rl_plan_bind_device_outputs(rl_plan* plan, int32_t which, const rl_out* dev_out);
-/* per-kernel device time of the last run, in ms, measured with HIP events on the
- * run stream (index 0 = main optimisation kernel, 1 = prepare, 2 = finalize).  */
+/* device time of the last run, in ms, measured with HIP events on the run stream:
+ * idx 0 = the whole run, 1 = the min-curvature kernel, 2 = the min-time kernel. */
 int rl_plan_kernel_ms(rl_plan* plan, int32_t idx, float* ms);
 int rl_plan_destroy(rl_plan* plan);
+
+/* ------------------------------------------------------- step 6: geometry
+ * pipeline::compute_geom_and_save (ref:1295-1335), the rows of <base>_with_geom.csv:
+ * the centreline spline evaluated at s_k = s0 + L*(k/denomN), heading, curvature,
+ * ray distances to the rings along ±n (distancesToRings, ref:513-524), width and
+ * v_kappa.  SURVEY §8f row 1. */
+
+/* centerline::Spline1D (ref:403-446): knots s[n], coefficients a,b,c,d [n] */
+typedef struct rl_spline {
+    const double* s;
+    const double* a;
+    const double* b;
+    const double* c;
+    const double* d;
+    int32_t n;
+    int32_t _pad;
+} rl_spline;
+
+typedef struct rl_geom_problem {
+    rl_spline spx, spy;          /* x(s), y(s) from splineUniformResample (ref:448-474)      */
+    double s0, L;                /* resample origin and length (ref:465)                      */
+    int32_t Kmax;                /* rows before the duplicate: closed ? samples : Ncenter (ref:1308) */
+    int32_t denomN;              /* closed ? samples : max(1, samples) (ref:1309)             */
+    int32_t emit_closed_duplicate; /* cfg emit_closed_duplicate: one more row (L, row 0) (ref:1331) */
+    int32_t closed;              /* ring segments are ringEdges (1) / polylineEdges (0) inputs */
+    const double* inner_seg;     /* [Ei][4] */
+    const double* outer_seg;     /* [Eo][4] */
+    int32_t Ei, Eo;
+} rl_geom_problem;
+
+#define RL_GEOM_COLS 9           /* s_rel,x,y,heading_rad,curvature,dist_to_inner,dist_to_outer,width,v_kappa_mps */
+
+/* Rows (Kmax + emit_closed_duplicate) x RL_GEOM_COLS into host `rows` (row-major),
+ * computed on `device`.  cfg supplies kappa_eps, a_lat_max, v_cap_mps.  *kernel_ms
+ * (optional) receives the HIP-event time of the geometry kernel.  Returns the row
+ * count or RL_E*. */
+int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double* rows, float* kernel_ms);
 
 /* ------------------------------------------------------------- runtime */
 int         rl_device_count(void);

@@ -521,6 +521,68 @@ int oracle_optimize(const rl_problem* pr, const rl_cfg* cfg, int32_t n_cfg, cons
     return oracle_optimize_range(pr, cfg, n_cfg, seeds, B, 0, B, out_mc, out_mt);
 }
 
+/* ---------------------------------------------------------- step 6: geometry */
+/* Spline1D::eval_with_deriv, ref:435-445 */
+static void spline_eval_d(const rl_spline* sp, double si, double* f, double* fp, double* fpp) {
+    const int n = sp->n;
+    if (n == 0) { *f = *fp = *fpp = 0; return; }
+    if (n == 1) { *f = sp->a[0]; *fp = *fpp = 0; return; }
+    int lo = 0, hi = n - 1;
+    if (si <= sp->s[0]) lo = 0;
+    else if (si >= sp->s[n - 1]) lo = n - 2;
+    else { while (hi - lo > 1) { int mid = (lo + hi) >> 1; if (sp->s[mid] <= si) lo = mid; else hi = mid; } }
+    double t = si - sp->s[lo];
+    *f = sp->a[lo] + sp->b[lo] * t + sp->c[lo] * t * t + sp->d[lo] * t * t * t;
+    *fp = sp->b[lo] + 2.0 * sp->c[lo] * t + 3.0 * sp->d[lo] * t * t;
+    *fpp = 2.0 * sp->c[lo] + 6.0 * sp->d[lo] * t;
+}
+/* distancesToRings, ref:513-524: per ring the nearer ray hit along ±n, else the
+ * point-to-segment minimum, non-finite -> 0 */
+static void dist_to_rings(double Px, double Py, double nx, double ny, const double* in, int Ei,
+                          const double* out, int Eo, double* d_in, double* d_out) {
+    double di1 = ray_ring(Px, Py, nx, ny, in, Ei), di2 = ray_ring(Px, Py, -nx, -ny, in, Ei);
+    *d_in = (isfinite(di1) || isfinite(di2)) ? smin(di1, di2) : min_dist_segs(Px, Py, in, Ei);
+    double do1 = ray_ring(Px, Py, nx, ny, out, Eo), do2 = ray_ring(Px, Py, -nx, -ny, out, Eo);
+    *d_out = (isfinite(do1) || isfinite(do2)) ? smin(do1, do2) : min_dist_segs(Px, Py, out, Eo);
+    if (!isfinite(*d_in)) *d_in = 0.0;
+    if (!isfinite(*d_out)) *d_out = 0.0;
+}
+/* pipeline::compute_geom_and_save rows, ref:1295-1335 (the CSV text is the caller's) */
+int oracle_geom(const rl_geom_problem* gp, const rl_cfg* C, double* rows) {
+    if (!gp || !C || !rows || gp->Kmax < 0 || gp->denomN == 0) return RL_EINVAL;
+    const int Kmax = gp->Kmax;
+    double r0[RL_GEOM_COLS] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < Kmax; ++k) {
+        double si = gp->s0 + gp->L * ((double)k / (double)gp->denomN);
+        double x, xp, xpp, y, yp, ypp;
+        spline_eval_d(&gp->spx, si, &x, &xp, &xpp);
+        spline_eval_d(&gp->spy, si, &y, &yp, &ypp);
+        double heading = atan2(yp, xp);
+        double speed2 = xp * xp + yp * yp;
+        double denom = pow(smax(1e-12, speed2), 1.5);
+        double curv = (xp * ypp - yp * xpp) / denom;
+        /* geom::normalize({-yp, xp}, 1e-12), ref:132 */
+        double vx = -yp, vy = xp, nn = sqrt(vx * vx + vy * vy), nx = 0.0, ny = 0.0;
+        if (!(nn < 1e-12)) { nx = vx / nn; ny = vy / nn; }
+        double d_in = 0.0, d_out = 0.0;
+        if (nx != 0 || ny != 0) dist_to_rings(x, y, nx, ny, gp->inner_seg, gp->Ei, gp->outer_seg, gp->Eo, &d_in, &d_out);
+        double width = d_in + d_out;
+        double denom_k = smax(fabs(curv), C->kappa_eps);
+        double v_kappa = sqrt(C->a_lat_max / denom_k);
+        if (v_kappa > C->v_cap_mps) v_kappa = C->v_cap_mps;
+        double* r = rows + RL_GEOM_COLS * k;
+        r[0] = si - gp->s0; r[1] = x; r[2] = y; r[3] = heading; r[4] = curv;
+        r[5] = d_in; r[6] = d_out; r[7] = width; r[8] = v_kappa;
+        if (k == 0) for (int j = 0; j < RL_GEOM_COLS; ++j) r0[j] = r[j];
+    }
+    if (gp->emit_closed_duplicate) {
+        double* r = rows + RL_GEOM_COLS * Kmax;
+        for (int j = 0; j < RL_GEOM_COLS; ++j) r[j] = r0[j];
+        r[0] = gp->L;
+    }
+    return Kmax + (gp->emit_closed_duplicate ? 1 : 0);
+}
+
 /* edges::ringEdges ref:251-255 / polylineEdges ref:256-260 */
 int oracle_ring_segments(const double* ring_xy, int32_t n, int32_t closed, double* seg_out) {
     if (n < 0 || (n > 0 && (!ring_xy || !seg_out))) return RL_EINVAL;

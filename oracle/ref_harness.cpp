@@ -220,6 +220,92 @@ int ref_vpass(const double* kappa, int N, double h, int closed, double* v, doubl
     return 0;
 }
 
+// Step 6, compute_geom_and_save (main.cpp:1295-1335), after steps 1-5 exactly as in
+// ref_prepare.  Exports the x(s)/y(s) splines (Spline1D s,a,b,c,d; main.cpp:403),
+// s0, L, the row count Kmax and the divisor denomN (main.cpp:1308-1309), the rings,
+// and full-precision rows [nrows][9] (s_rel,x,y,heading,curvature,d_in,d_out,width,
+// v_kappa) computed with the reference's own functions in the reference's order,
+// plus the closed-duplicate row when emit_closed_duplicate.  The reference's own
+// writer runs as well and leaves <out_csv base>_with_geom.csv next to out_csv.
+int ref_geom(const char* inner_path, const char* outer_path, const char* out_csv,
+             double* knots, int knot_cap, int* nknots_out, double* s0_out, double* L_out,
+             int* Kmax_out, int* denomN_out, int* closed_out,
+             double* inner_xy, int* Ni_out, double* outer_xy, int* No_out, int ring_cap,
+             double* rows, int row_cap, int* nrows_out) {
+    CerrMute mute;
+    try {
+        auto& C = cfg::get();
+        const string base = io::dropExt(out_csv);
+        auto inner = io::loadCSV_XY(inner_path);
+        auto outer = io::loadCSV_XY(outer_path);
+        if (inner.size() < 2 || outer.size() < 2) { g_err = "need >=2 points per ring"; return -2; }
+        const bool closed_mode = C.is_closed_track;
+        auto tri = pipeline::buildDT(inner, outer);
+        auto MF = pipeline::extract_mids_with_len_filter(tri, base);
+        if (C.use_dynamic_samples) C.samples = pipeline::dynamic_samples_from_mids_count((int)MF.mids.size());
+        auto OM = pipeline::order_and_align_mids_open_closed(MF.mids, closed_mode);
+        auto RR = pipeline::reconstruct_rings_and_align(OM, MF, tri, base);
+        auto CL = pipeline::make_centerline(OM, closed_mode, base);
+        pipeline::compute_geom_and_save(base, CL.center, CL.spx, CL.spy, CL.s0, CL.L, closed_mode,
+                                        RR.inner_from_mids, RR.outer_from_mids);
+        const int nk = (int)CL.spx.s.size();
+        if (nk > knot_cap || (int)CL.spy.s.size() != nk || (int)RR.inner_from_mids.size() > ring_cap ||
+            (int)RR.outer_from_mids.size() > ring_cap) { g_err = "capacity"; return -3; }
+        const vector<double>* arr[10] = {&CL.spx.s, &CL.spx.a, &CL.spx.b, &CL.spx.c, &CL.spx.d,
+                                         &CL.spy.s, &CL.spy.a, &CL.spy.b, &CL.spy.c, &CL.spy.d};
+        for (int j = 0; j < 10; ++j)
+            for (int i = 0; i < nk; ++i) knots[j * knot_cap + i] = (*arr[j])[i];
+        *nknots_out = nk;
+        *s0_out = CL.s0;
+        *L_out = CL.L;
+        const int Ncenter = (int)CL.center.size();
+        const int Kmax = closed_mode ? C.samples : Ncenter;
+        const int denomN = closed_mode ? C.samples : std::max(1, C.samples);
+        *Kmax_out = Kmax;
+        *denomN_out = denomN;
+        *closed_out = closed_mode ? 1 : 0;
+        *Ni_out = (int)RR.inner_from_mids.size();
+        *No_out = (int)RR.outer_from_mids.size();
+        for (int i = 0; i < *Ni_out; ++i) { inner_xy[2 * i] = RR.inner_from_mids[i].x; inner_xy[2 * i + 1] = RR.inner_from_mids[i].y; }
+        for (int i = 0; i < *No_out; ++i) { outer_xy[2 * i] = RR.outer_from_mids[i].x; outer_xy[2 * i + 1] = RR.outer_from_mids[i].y; }
+        // the rows, with the reference's functions (main.cpp:1297-1335)
+        SegVec innerE = closed_mode ? edges::ringEdges(RR.inner_from_mids) : edges::polylineEdges(RR.inner_from_mids);
+        SegVec outerE = closed_mode ? edges::ringEdges(RR.outer_from_mids) : edges::polylineEdges(RR.outer_from_mids);
+        const int nrows = Kmax + (C.emit_closed_duplicate ? 1 : 0);
+        if (nrows > row_cap) { g_err = "row capacity"; return -3; }
+        for (int k = 0; k < Kmax; ++k) {
+            double si = CL.s0 + CL.L * (double(k) / double(denomN));
+            double x, xp, xpp, y, yp, ypp;
+            CL.spx.eval_with_deriv(si, x, xp, xpp);
+            CL.spy.eval_with_deriv(si, y, yp, ypp);
+            double heading = std::atan2(yp, xp);
+            double speed2 = xp * xp + yp * yp;
+            double denom = std::pow(std::max(1e-12, speed2), 1.5);
+            double curv = (xp * ypp - yp * xpp) / denom;
+            Vec2 nvec = geom::normalize(Vec2{-yp, xp}, 1e-12);
+            double d_in = 0.0, d_out = 0.0;
+            if (nvec.x != 0 || nvec.y != 0) distancesToRings({x, y}, nvec, innerE, outerE, d_in, d_out);
+            double width = d_in + d_out;
+            double denom_k = std::max(std::fabs(curv), C.kappa_eps);
+            double v_kappa = std::sqrt(C.a_lat_max / denom_k);
+            if (v_kappa > C.v_cap_mps) v_kappa = C.v_cap_mps;
+            double* r = rows + 9 * k;
+            r[0] = si - CL.s0; r[1] = x; r[2] = y; r[3] = heading; r[4] = curv;
+            r[5] = d_in; r[6] = d_out; r[7] = width; r[8] = v_kappa;
+        }
+        if (C.emit_closed_duplicate) {
+            double* r = rows + 9 * Kmax;
+            for (int j = 0; j < 9; ++j) r[j] = (Kmax > 0) ? rows[j] : 0.0;
+            r[0] = CL.L;
+        }
+        *nrows_out = nrows;
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 // Whole reference CLI (main.cpp:1598) — used to produce the reference's own CSV
 // files for the output-format contract fixtures.
 int ref_run_cli(const char* inner_path, const char* outer_path, const char* out_csv) {

@@ -238,6 +238,63 @@ class Outputs:
         return o
 
 
+class RlSpline(C.Structure):
+    """centerline::Spline1D (ref:403-446)."""
+    _fields_ = [("s", C.POINTER(C.c_double)), ("a", C.POINTER(C.c_double)), ("b", C.POINTER(C.c_double)),
+                ("c", C.POINTER(C.c_double)), ("d", C.POINTER(C.c_double)), ("n", C.c_int32), ("_pad", C.c_int32)]
+
+
+class RlGeomProblem(C.Structure):
+    """Inputs of pipeline::compute_geom_and_save (ref:1288-1335)."""
+    _fields_ = [("spx", RlSpline), ("spy", RlSpline), ("s0", C.c_double), ("L", C.c_double),
+                ("Kmax", C.c_int32), ("denomN", C.c_int32), ("emit_closed_duplicate", C.c_int32),
+                ("closed", C.c_int32), ("inner_seg", C.POINTER(C.c_double)), ("outer_seg", C.POINTER(C.c_double)),
+                ("Ei", C.c_int32), ("Eo", C.c_int32)]
+
+
+RL_GEOM_COLS = 9
+GEOM_COLS = ("s", "x", "y", "heading_rad", "curvature", "dist_to_inner", "dist_to_outer", "width", "v_kappa_mps")
+
+
+@dataclass
+class GeomProblem:
+    """Step 6 inputs: the x(s), y(s) splines as knots [10][n] (x: s,a,b,c,d then y:
+    s,a,b,c,d), s0, L, Kmax, denomN (ref:1308-1309), ring segments [E,4]."""
+
+    knots: np.ndarray
+    s0: float
+    L: float
+    Kmax: int
+    denomN: int
+    inner_seg: np.ndarray
+    outer_seg: np.ndarray
+    closed: bool = True
+    emit_closed_duplicate: bool = True
+
+    def __post_init__(self):
+        self.knots = np.ascontiguousarray(self.knots, dtype=np.float64).reshape(10, -1)
+        self.inner_seg = np.ascontiguousarray(self.inner_seg, dtype=np.float64).reshape(-1, 4)
+        self.outer_seg = np.ascontiguousarray(self.outer_seg, dtype=np.float64).reshape(-1, 4)
+
+    @property
+    def rows(self) -> int:
+        return int(self.Kmax) + (1 if self.emit_closed_duplicate else 0)
+
+    def as_c(self) -> RlGeomProblem:
+        g = RlGeomProblem()
+        n = self.knots.shape[1]
+        for sp, off in ((g.spx, 0), (g.spy, 5)):
+            sp.s, sp.a, sp.b, sp.c, sp.d = (dptr(self.knots[off + j]) for j in range(5))
+            sp.n = n
+        g.s0, g.L = float(self.s0), float(self.L)
+        g.Kmax, g.denomN = int(self.Kmax), int(self.denomN)
+        g.emit_closed_duplicate = 1 if self.emit_closed_duplicate else 0
+        g.closed = 1 if self.closed else 0
+        g.inner_seg, g.outer_seg = dptr(self.inner_seg), dptr(self.outer_seg)
+        g.Ei, g.Eo = self.inner_seg.shape[0], self.outer_seg.shape[0]
+        return g
+
+
 def cfg_array(cfgs) -> tuple:
     """list of RlCfg (or one) -> (ctypes array, n)."""
     if isinstance(cfgs, RlCfg):
@@ -304,6 +361,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_abi_version.restype = C.c_int
     lib.rl_kernel_variant.argtypes = [C.c_int32]
     lib.rl_kernel_variant.restype = C.c_int
+    lib.rl_geom.argtypes = [C.POINTER(RlGeomProblem), C.POINTER(RlCfg), C.c_int32, C.POINTER(C.c_double),
+                            C.POINTER(C.c_float)]
+    lib.rl_geom.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib
     return lib

@@ -385,6 +385,108 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
     return RL_OK;
 }
 
+// pipeline::compute_geom_and_save rows (ref:1295-1335) on the device
+int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double* rows, float* kernel_ms) {
+    if (!gp || !cfg || !rows) return fail(RL_EINVAL, "rl_geom: NULL argument");
+    if (gp->Kmax < 0 || gp->denomN == 0) return fail(RL_EINVAL, "rl_geom: Kmax < 0 or denomN == 0");
+    if (gp->spx.n != gp->spy.n || gp->spx.n < 0) return fail(RL_EINVAL, "rl_geom: spline sizes differ");
+    if (gp->Ei < 0 || gp->Eo < 0 || (gp->Ei > 0 && !gp->inner_seg) || (gp->Eo > 0 && !gp->outer_seg))
+        return fail(RL_EINVAL, "rl_geom: bad segments");
+    const int nk = gp->spx.n;
+    const rl_spline* sp[2] = {&gp->spx, &gp->spy};
+    for (int a = 0; a < 2; ++a)
+        if (nk > 0 && (!sp[a]->s || !sp[a]->a || !sp[a]->b || !sp[a]->c || !sp[a]->d))
+            return fail(RL_EINVAL, "rl_geom: NULL spline array");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    const int nrows = gp->Kmax + (gp->emit_closed_duplicate ? 1 : 0);
+    if (gp->Kmax == 0) {                      // no rows computed: the duplicate is (L, 0, ..., 0)
+        if (nrows) { std::memset(rows, 0, sizeof(double) * RL_GEOM_COLS); rows[0] = gp->L; }
+        if (kernel_ms) *kernel_ms = 0.0f;
+        return nrows;
+    }
+    RingHost rh[2] = {make_ring(gp->inner_seg, gp->Ei), make_ring(gp->outer_seg, gp->Eo)};
+    std::vector<double> kn((size_t)10 * std::max(nk, 1), 0.0);
+    for (int a = 0; a < 2; ++a) {
+        const double* arr[5] = {sp[a]->s, sp[a]->a, sp[a]->b, sp[a]->c, sp[a]->d};
+        for (int j = 0; j < 5; ++j)
+            if (nk) std::memcpy(&kn[(size_t)(5 * a + j) * nk], arr[j], sizeof(double) * nk);
+    }
+    const size_t Mt = (size_t)rh[0].M + rh[1].M;
+    std::vector<void*> mem;
+    auto dalloc = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+        mem.push_back(p);
+        return p;
+    };
+    auto release = [&](int code) {
+        for (void* p : mem) hipFree(p);
+        return code;
+    };
+    double* d_kn = (double*)dalloc(kn.size() * sizeof(double));
+    double* d_vtx = (double*)dalloc(2 * Mt * sizeof(double));
+    rl::SegRec* d_rec = (rl::SegRec*)dalloc(Mt * sizeof(rl::SegRec));
+    uint32_t* d_flag = (uint32_t*)dalloc(Mt / 32 * sizeof(uint32_t));
+    double* d_rows = (double*)dalloc((size_t)nrows * RL_GEOM_COLS * sizeof(double));
+    if (!d_kn || !d_vtx || !d_rec || !d_flag || !d_rows) return release(fail(RL_ENOMEM, "rl_geom: hipMalloc failed"));
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return release(fail(RL_EHIP, "rl_geom: stream"));
+    auto finish = [&](int code) {
+        if (e0) hipEventDestroy(e0);
+        if (e1) hipEventDestroy(e1);
+        hipStreamSynchronize(st);
+        hipStreamDestroy(st);
+        return release(code);
+    };
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return finish(fail(RL_EHIP, "rl_geom: events"));
+    if (hipMemcpyAsync(d_kn, kn.data(), kn.size() * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
+        return finish(fail(RL_EHIP, "rl_geom: upload knots"));
+    rl::GeomParams g{};
+    for (int r = 0, off = 0; r < 2; off += rh[r].M, ++r) {
+        const RingHost& R = rh[r];
+        if (R.M) {
+            if (hipMemcpyAsync(d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice, st) ||
+                hipMemcpyAsync(d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st) ||
+                hipMemcpyAsync(d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st))
+                return finish(fail(RL_EHIP, "rl_geom: upload rings"));
+        }
+        g.ring[r].vtx = (const double2*)(d_vtx + 2 * (size_t)off);
+        g.ring[r].rec = d_rec + off;
+        g.ring[r].flag = d_flag + off / 32;
+        g.ring[r].M = R.M;
+        g.ring[r].E = R.E;
+        g.ring[r].dl0 = R.dl0;
+    }
+    g.kx = d_kn;
+    g.ky = d_kn + 5 * (size_t)nk;
+    g.nk = nk;
+    g.Kmax = gp->Kmax;
+    g.denomN = gp->denomN;
+    g.emit_dup = gp->emit_closed_duplicate ? 1 : 0;
+    g.s0 = gp->s0;
+    g.L = gp->L;
+    g.kappa_eps = cfg->kappa_eps;
+    g.a_lat_max = cfg->a_lat_max;
+    g.v_cap = cfg->v_cap_mps;
+    g.rows = d_rows;
+    if (hipEventRecord(e0, st) != hipSuccess) return finish(fail(RL_EHIP, "rl_geom: event"));
+    if (rl::launch_geom(g, st) != hipSuccess) return finish(fail(RL_EHIP, "rl_geom: kernel launch"));
+    if (hipEventRecord(e1, st) != hipSuccess) return finish(fail(RL_EHIP, "rl_geom: event"));
+    if (hipMemcpyAsync(rows, d_rows, (size_t)nrows * RL_GEOM_COLS * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return finish(fail(RL_EHIP, "rl_geom: download"));
+    if (kernel_ms) {
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e0, e1);
+        *kernel_ms = ms;
+    }
+    return finish(nrows);
+}
+
 int rl_plan_kernel_ms(rl_plan* p, int32_t idx, float* ms) {
     if (!p || !ms || !p->ran) return fail(RL_EINVAL, "plan not run");
     HIPCHK(hipSetDevice(p->device));

@@ -39,6 +39,18 @@ int pick_k(int N);
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
 // large-N variant: one 1024-thread workgroup per instance, state in HBM
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st);
+// step 6 geometry (rl_geom.hip): spline knots [5][nk] per axis (s,a,b,c,d), rows [Kmax+dup][9]
+struct GeomParams {
+    const double* kx;
+    const double* ky;
+    int32_t nk;
+    int32_t Kmax, denomN, emit_dup;
+    double s0, L;
+    RingDesc ring[2];
+    double kappa_eps, a_lat_max, v_cap;
+    double* rows;
+};
+hipError_t launch_geom(const GeomParams& g, hipStream_t st);
 #ifdef RL_STAMPS
 int debug_stamps(unsigned long long* host, int nblocks);
 #endif

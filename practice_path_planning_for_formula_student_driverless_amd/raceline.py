@@ -30,7 +30,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import abi
-from .abi import Outputs, Problem, RlCfg, default_cfg, set_mu  # noqa: F401
+from .abi import GeomProblem, Outputs, Problem, RlCfg, default_cfg, set_mu  # noqa: F401
 
 
 class RacelineError(RuntimeError):
@@ -288,6 +288,44 @@ def compute_mintime_and_save(base: str, center_for_opt, s0: float, L: float, clo
     import sys
     sys.stderr.write(f"[mintime] Estimated laptime: {res.lap_time:.3f} s\n")
     return res
+
+
+# ------------------------------------------------------- step 6: geometry
+GEOM_HEADER = "s,x,y,heading_rad,curvature,dist_to_inner,dist_to_outer,width,v_kappa_mps\n"
+
+
+def format_geom_csv(rows: np.ndarray) -> str:
+    """<base>_with_geom.csv text of pipeline::compute_geom_and_save (ref:1300-1334):
+    header, then every row with std::fixed / precision(9)."""
+    out = [GEOM_HEADER]
+    for r in np.asarray(rows, dtype=np.float64).reshape(-1, 9):
+        out.append(",".join(_f9(v) for v in r) + "\n")
+    return "".join(out)
+
+
+def compute_geom(gp: GeomProblem, cfg: Optional[RlCfg] = None, device: int = 0, return_ms: bool = False):
+    """Rows of pipeline::compute_geom_and_save (ref:1295-1335) on the GPU (rl_geom):
+    [Kmax + emit_closed_duplicate, 9] = s_rel, x, y, heading, curvature, d_in, d_out,
+    width, v_kappa.  Fails loudly without a device (no CPU path)."""
+    lib = _lib()
+    cfg = cfg if cfg is not None else default_cfg()
+    rows = np.zeros((max(gp.rows, 1), 9))
+    g = gp.as_c()
+    ms = C.c_float(0.0)
+    n = lib.rl_geom(C.byref(g), C.byref(cfg), int(device), rows.ctypes.data_as(C.POINTER(C.c_double)),
+                    C.byref(ms))
+    if n < 0:
+        raise RacelineError(n, lib.rl_last_error().decode())
+    rows = rows[:n]
+    return (rows, float(ms.value)) if return_ms else rows
+
+
+def compute_geom_and_save(base: str, gp: GeomProblem, cfg: Optional[RlCfg] = None, device: int = 0) -> np.ndarray:
+    """pipeline::compute_geom_and_save (ref:1288-1335): writes <base>_with_geom.csv."""
+    rows = compute_geom(gp, cfg, device)
+    with open(base + "_with_geom.csv", "w") as f:
+        f.write(format_geom_csv(rows))
+    return rows
 
 
 def load_csv_xy(path: str) -> np.ndarray:

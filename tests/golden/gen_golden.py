@@ -16,6 +16,10 @@ Cases:
   sweep_*               competition_map1 default N, (mu, P_max_W, lambda_smooth) grid corners,
                         time_weight_use_inv_v / use_total_ge_lat variants; both modes
   oval_n10000           synthetic oval, samples=10000 (C5); both modes
+  geom_<case>           step 6 (compute_geom_and_save, main.cpp:1295-1335): splines, rings and the
+                        full-precision rows, plus the reference's own <base>_with_geom.csv text
+                        (7 tracks, training_map open, competition_map1 samples=2000);
+                        `gen_golden.py --geom` regenerates only these
 Known answers recorded in manifest.json:
   shuffled_identical    *_shuffled.csv inputs give bit-identical hot-path inputs
   error_path            csv/inner.csv+outer.csv -> "not enough midpoints after length filter"
@@ -85,6 +89,27 @@ class Ref:
                     inner_ring=inn[: 2 * Ni.value].reshape(-1, 2).copy(),
                     outer_ring=out[: 2 * No.value].reshape(-1, 2).copy(), samples=S.value)
 
+    def geom(self, inner, outer, csv_dir, tag):
+        cap, rcap, rowcap = 20000, 5000, 20002
+        knots = np.zeros(10 * cap)
+        inn, out = np.zeros(2 * rcap), np.zeros(2 * rcap)
+        rows = np.zeros(9 * rowcap)
+        nk, K, dN, cl, Ni, No, nr = (C.c_int() for _ in range(7))
+        s0, L = C.c_double(), C.c_double()
+        base = os.path.join(self.tmp, f"g_{tag}.csv")
+        rc = self.lib.ref_geom(inner.encode(), outer.encode(), base.encode(), vp(knots), cap, C.byref(nk),
+                               C.byref(s0), C.byref(L), C.byref(K), C.byref(dN), C.byref(cl), vp(inn), C.byref(Ni),
+                               vp(out), C.byref(No), rcap, vp(rows), rowcap, C.byref(nr))
+        if rc != 0:
+            raise RuntimeError(self.lib.ref_last_error().decode())
+        kn = knots.reshape(10, cap)[:, : nk.value].copy()
+        shutil.copy(os.path.join(self.tmp, f"g_{tag}_with_geom.csv"), os.path.join(csv_dir, f"geom_{tag}.csv"))
+        return dict(knots=kn, s0=np.float64(s0.value), L=np.float64(L.value), Kmax=np.int64(K.value),
+                    denomN=np.int64(dN.value), closed=np.int64(cl.value),
+                    inner_ring=inn[: 2 * Ni.value].reshape(-1, 2).copy(),
+                    outer_ring=out[: 2 * No.value].reshape(-1, 2).copy(),
+                    rows=rows[: 9 * nr.value].reshape(-1, 9).copy())
+
     def segs(self, ring, closed):
         seg = np.zeros(4 * max(len(ring), 1))
         r = np.ascontiguousarray(ring, dtype=np.float64)
@@ -124,7 +149,38 @@ def write_oval(d):
     return paths
 
 
+def geom_fixtures(ref, manifest):
+    """Step-6 fixtures."""
+    csv_dir = os.path.join(HERE, "ref_csv")
+    os.makedirs(csv_dir, exist_ok=True)
+    manifest["geom_cases"] = {}
+    todo = [(tr, f"{REF_CSV}/{tr}_inner.csv", f"{REF_CSV}/{tr}_outer.csv", True, None) for tr in TRACKS]
+    todo += [("training_open", f"{REF_CSV}/training_map_inner.csv", f"{REF_CSV}/training_map_outer.csv", False, None),
+             ("cmap1_n2000", f"{REF_CSV}/competition_map1_inner.csv", f"{REF_CSV}/competition_map1_outer.csv", True, 2000)]
+    for tag, inner, outer, closed, samples in todo:
+        ref.reset()
+        ref.lib.ref_set_closed(1 if closed else 0)
+        if samples:
+            ref.lib.ref_set_sampling(0, samples)
+        cfg = ref.cfg()
+        d = ref.geom(inner, outer, csv_dir, tag)
+        fname = f"geom_{tag}.npz"
+        np.savez_compressed(os.path.join(HERE, fname), **d)
+        manifest["geom_cases"][tag] = {"file": fname, "csv": f"ref_csv/geom_{tag}.csv", "rows": int(d["rows"].shape[0]),
+                                       "knots": int(d["knots"].shape[1]), "closed": bool(closed), "cfg": cfg.to_dict()}
+        print("geom", tag, d["rows"].shape, d["knots"].shape)
+
+
 def main():
+    if "--geom" in sys.argv:
+        ref = Ref()
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        geom_fixtures(ref, manifest)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        shutil.rmtree(ref.tmp, ignore_errors=True)
+        return
     ref = Ref()
     manifest = {"generator": "tests/golden/gen_golden.py", "reference": "src/main.cpp sha256 e7820e5852246581...",
                 "cases": {}, "known_answers": {}}
@@ -228,6 +284,7 @@ def main():
     for suffix in ("_raceline.csv", "_raceline_with_geom.csv", "_mintime_raceline.csv", "_mintime_with_geom.csv"):
         shutil.copy(os.path.join(cli_dir, "training_map_centerline" + suffix), os.path.join(csv_dir, "training_map" + suffix))
     manifest["ref_csv"] = {"track": "training_map", "dir": "ref_csv"}
+    geom_fixtures(ref, manifest)
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

@@ -45,6 +45,8 @@ def oracle() -> C.CDLL:
         lib.oracle_vpass.restype = C.c_double
         lib.oracle_ring_segments.argtypes = [C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_double)]
         lib.oracle_ring_segments.restype = C.c_int
+        lib.oracle_geom.argtypes = [C.POINTER(abi.RlGeomProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double)]
+        lib.oracle_geom.restype = C.c_int
         _ORACLE = lib
     return _ORACLE
 
@@ -110,3 +112,34 @@ def manifest() -> dict:
 
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)
+
+
+# ------------------------------------------------------------ step 6 (geometry)
+def load_geom_case(name: str) -> dict:
+    meta = manifest()["geom_cases"][name]
+    with np.load(os.path.join(GOLDEN, meta["file"]), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["_meta"] = meta
+    with open(os.path.join(GOLDEN, meta["csv"]), "rb") as f:
+        d["_csv"] = f.read()
+    return d
+
+
+def geom_problem(case: dict) -> abi.GeomProblem:
+    closed = bool(case["closed"])
+    return abi.GeomProblem(knots=case["knots"], s0=float(case["s0"]), L=float(case["L"]), Kmax=int(case["Kmax"]),
+                           denomN=int(case["denomN"]), inner_seg=ring_segments(case["inner_ring"], closed),
+                           outer_seg=ring_segments(case["outer_ring"], closed), closed=closed,
+                           emit_closed_duplicate=True)
+
+
+def geom_cfg(case: dict) -> abi.RlCfg:
+    return abi.RlCfg.from_dict(case["_meta"]["cfg"])
+
+
+def run_oracle_geom(gp: abi.GeomProblem, cfg: abi.RlCfg) -> np.ndarray:
+    rows = np.zeros((max(gp.rows, 1), abi.RL_GEOM_COLS))
+    g = gp.as_c()
+    n = oracle().oracle_geom(C.byref(g), C.byref(cfg), rows.ctypes.data_as(C.POINTER(C.c_double)))
+    assert n == gp.rows, n
+    return rows[: gp.rows]

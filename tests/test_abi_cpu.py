@@ -34,7 +34,7 @@ def test_header_declares_expected_entry_points():
     for must in ("rl_optimize", "rl_plan_create", "rl_plan_run", "rl_plan_fetch", "rl_plan_destroy",
                  "rl_plan_device_outputs", "rl_plan_kernel_ms", "rl_plan_bind_device_outputs", "rl_cfg_default", "rl_cfg_set_mu",
                  "rl_ring_segments", "rl_seed_value", "rl_device_count", "rl_last_error", "rl_abi_version",
-                 "rl_kernel_variant"):
+                 "rl_kernel_variant", "rl_geom"):
         assert must in names
 
 
@@ -58,6 +58,8 @@ int main(void){
          offsetof(rl_cfg, inv_v_gain), offsetof(rl_cfg, use_total_ge_lat));
   printf("%zu %zu %zu\n", offsetof(rl_problem, L), offsetof(rl_problem, outer_seg), offsetof(rl_problem, veh_width));
   printf("%zu\n", offsetof(rl_out, vpass_sweeps));
+  printf("%zu %zu %zu %zu %zu\n", sizeof(rl_spline), sizeof(rl_geom_problem), offsetof(rl_geom_problem, s0),
+         offsetof(rl_geom_problem, inner_seg), offsetof(rl_geom_problem, Eo));
   return 0;
 }'''
     with tempfile.TemporaryDirectory() as d:
@@ -71,6 +73,8 @@ int main(void){
                          abi.RlCfg.inv_v_gain.offset, abi.RlCfg.use_total_ge_lat.offset]
     assert vals[7:10] == [abi.RlProblem.L.offset, abi.RlProblem.outer_seg.offset, abi.RlProblem.veh_width.offset]
     assert vals[10] == abi.RlOut.vpass_sweeps.offset
+    assert vals[11:16] == [C.sizeof(abi.RlSpline), C.sizeof(abi.RlGeomProblem), abi.RlGeomProblem.s0.offset,
+                           abi.RlGeomProblem.inner_seg.offset, abi.RlGeomProblem.Eo.offset]
 
 
 def test_cfg_default_equals_reference_defaults():
@@ -119,6 +123,10 @@ def test_compute_fails_loudly_without_gpu():
     case = O.load_case("track_training_map")
     with pytest.raises(raceline.RacelineError) as ei:
         raceline.optimize_batch(O.case_problem(case), O.case_cfg(case), None, 1)
+    assert ei.value.code == abi.RL_ENODEV
+    g = O.load_geom_case("training_map")
+    with pytest.raises(raceline.RacelineError) as ei:
+        raceline.compute_geom(O.geom_problem(g), O.geom_cfg(g))
     assert ei.value.code == abi.RL_ENODEV
 
 

@@ -310,6 +310,56 @@ def test_streaming_kernel_golden_tracks(monkeypatch):
         assert abs(mt.lap[0] - float(case["mt_lap"])) / float(case["mt_lap"]) <= REL
 
 
+GEOM = list(O.manifest().get("geom_cases", {}))
+
+
+@pytest.mark.parametrize("name", GEOM)
+def test_geom_vs_reference(name):
+    """Step 6 (compute_geom_and_save, ref:1295-1335) on the GPU vs the reference's
+    full-precision rows and its own <base>_with_geom.csv bytes."""
+    _lib_or_skip()
+    case = O.load_geom_case(name)
+    gp, cfg = O.geom_problem(case), O.geom_cfg(case)
+    rows = raceline.compute_geom(gp, cfg)
+    ref = case["rows"]
+    assert rows.shape == ref.shape
+    for j, col in enumerate(abi.GEOM_COLS):
+        col_close(rows[:, j], ref[:, j], f"geom.{name}.{col}")
+        zero_signs_equal(rows[:, j], ref[:, j], f"geom.{name}.{col}")
+    # every column except heading (OCML atan2) and curvature (pow15) is bit-identical
+    for j in (0, 1, 2, 5, 6, 7):
+        np.testing.assert_array_equal(rows[:, j], ref[:, j], err_msg=f"geom.{name}.{abi.GEOM_COLS[j]}")
+    assert raceline.format_geom_csv(rows).encode() == case["_csv"]
+
+
+def test_geom_segment_lists_and_edges():
+    """Step 6 on shuffled / split / empty rings and Kmax edge cases vs the oracle."""
+    _lib_or_skip()
+    rng = np.random.default_rng(3)
+    case = O.load_geom_case("competition_map2")
+    base, cfg = O.geom_problem(case), O.geom_cfg(case)
+    for which in ("inner", "outer"):
+        for vname, seg in _segment_variants(getattr(base, f"{which}_seg"), rng).items():
+            kw = dict(knots=base.knots, s0=base.s0, L=base.L, Kmax=base.Kmax, denomN=base.denomN,
+                      inner_seg=base.inner_seg, outer_seg=base.outer_seg, closed=base.closed)
+            kw[f"{which}_seg"] = seg
+            gp = abi.GeomProblem(**kw)
+            rows = raceline.compute_geom(gp, cfg)
+            orc = O.run_oracle_geom(gp, cfg)
+            for j, col in enumerate(abi.GEOM_COLS):
+                col_close(rows[:, j], orc[:, j], f"geom.{which}.{vname}.{col}")
+            np.testing.assert_array_equal(rows[:, 5:8], orc[:, 5:8], err_msg=f"geom.{which}.{vname}.dist")
+    for K in (0, 1, 255, 256, 257):
+        gp = abi.GeomProblem(knots=base.knots, s0=base.s0, L=base.L, Kmax=K, denomN=max(K, 1),
+                             inner_seg=base.inner_seg, outer_seg=base.outer_seg, closed=True)
+        rows = raceline.compute_geom(gp, cfg)
+        orc = O.run_oracle_geom(gp, cfg)
+        assert rows.shape == orc.shape == (K + 1, 9)
+        np.testing.assert_array_equal(rows[:, 5:8], orc[:, 5:8])
+        for j in range(9):
+            col_close(rows[:, j], orc[:, j], f"geom.K{K}.{j}")
+
+
 def test_errors_fail_loudly():
     _lib_or_skip()
     case = O.load_case("track_training_map")

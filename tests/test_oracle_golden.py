@@ -125,3 +125,22 @@ def test_vpass_early_exit_is_exact():
     np.testing.assert_array_equal(v20, vS)
     assert lap20 == lapS
     assert cfg.max_vpass_iters == 6 and 1 <= s20 <= 6
+
+
+# ------------------------------------------------------------ step 6 (geometry)
+GEOM = list(O.manifest().get("geom_cases", {}))
+
+
+@pytest.mark.parametrize("name", GEOM)
+def test_geom_oracle_bit_exact(name):
+    """oracle_geom == the reference's compute_geom_and_save rows bit for bit, and both
+    format to the reference's own <base>_with_geom.csv byte for byte."""
+    from practice_path_planning_for_formula_student_driverless_amd import raceline
+    case = O.load_geom_case(name)
+    gp = O.geom_problem(case)
+    rows = O.run_oracle_geom(gp, O.geom_cfg(case))
+    np.testing.assert_array_equal(rows, case["rows"])
+    assert np.array_equal(np.signbit(rows), np.signbit(case["rows"]))
+    text = raceline.format_geom_csv(case["rows"]).encode()
+    assert text == case["_csv"]
+    assert raceline.format_geom_csv(rows).encode() == case["_csv"]
