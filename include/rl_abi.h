@@ -185,6 +185,16 @@ int rl_plan_bind_device_outputs(rl_plan* plan, int32_t which, const rl_out* dev_
 int rl_plan_kernel_ms(rl_plan* plan, int32_t idx, float* ms);
 int rl_plan_destroy(rl_plan* plan);
 
+/* B lap evaluations of given paths: heading/curvature
+ * (heading_curv_from_points_generic, ref:595-620) and velocity_profile_forward_backward
+ * (ref:782-862) with h = L[b]/N on path b — the min-time driver's final step
+ * (ref:1045-1048) and the debug dump's centreline / min-curvature laps (ref:1466-1478),
+ * i.e. compute_min_time_raceline with max_outer_iters = 0.  paths_xy [B][N][2], L [B];
+ * `out` receives heading, kappa, v, ax, lap and vpass_sweeps [B][1] (x, y echo the path,
+ * alphas are 0); evals/accepts may be NULL.  cfg[n_cfg] as in rl_optimize. */
+int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, int32_t closed,
+                const rl_cfg* cfg, int32_t n_cfg, int32_t device, rl_out* out);
+
 /* ------------------------------------------------------- step 6: geometry
  * pipeline::compute_geom_and_save (ref:1295-1335), the rows of <base>_with_geom.csv:
  * the centreline spline evaluated at s_k = s0 + L*(k/denomN), heading, curvature,

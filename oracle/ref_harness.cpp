@@ -122,6 +122,20 @@ void ref_set_sampling(int use_dynamic, int samples) {
     cfg::get().samples = samples;
 }
 void ref_set_closed(int closed) { cfg::get().is_closed_track = closed != 0; }
+void ref_set_debug(int on) { cfg::get().debug_dump = on != 0; }
+
+// heading_curv_from_points_generic + velocity_profile_forward_backward on a path with
+// a given h (main.cpp:1466-1478: the debug dump's centreline / min-curvature laps).
+int ref_lap_eval(const double* path_xy, int N, double h, int closed, double* heading, double* kappa, double* v,
+                 double* ax, double* lap) {
+    auto P = pts_from(path_xy, N);
+    vector<double> hd, kp;
+    raceline_min_curv::heading_curv_from_points_generic(P, h, closed != 0, hd, kp);
+    auto VP = raceline_min_time::velocity_profile_forward_backward(kp, h, closed != 0);
+    for (int i = 0; i < N; ++i) { heading[i] = hd[i]; kappa[i] = kp[i]; v[i] = VP.v[i]; ax[i] = VP.ax[i]; }
+    *lap = VP.lap_time;
+    return 0;
+}
 
 // Steps 1-6 of main (main.cpp:1617-1693) up to the hot-path inputs.
 // Capacities: center_cap points, ring_cap points per ring.  Returns 0 or -1.

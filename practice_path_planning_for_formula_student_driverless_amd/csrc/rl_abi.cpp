@@ -120,6 +120,8 @@ struct rl_plan {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran = false;
     double* d_center = nullptr;
+    double* d_Ls = nullptr;           // per-instance L (lap evaluation) or nullptr
+    int64_t center_stride = 0;        // doubles between instances' centres (0: shared)
     double* d_vtx = nullptr;
     rl::SegRec* d_rec = nullptr;
     uint32_t* d_flag = nullptr;
@@ -236,8 +238,18 @@ int rl_plan_destroy(rl_plan* plan) {
     return RL_OK;
 }
 
+// rl_plan_create with optional per-instance centres [B][N][2] and lengths [B]
+// (centers/Ls non-NULL: prob->center_xy and prob->L are ignored)
+static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
+                          const uint64_t* seeds, int32_t B, int32_t modes, const double* centers, const double* Ls);
+
 int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
                    const uint64_t* seeds, int32_t B, int32_t modes) {
+    return plan_create_ex(out, device, prob, cfg, n_cfg, seeds, B, modes, nullptr, nullptr);
+}
+
+static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
+                          const uint64_t* seeds, int32_t B, int32_t modes, const double* centers, const double* Ls) {
     if (!out) return fail(RL_EINVAL, "plan out pointer is NULL");
     *out = nullptr;
     if (!prob || !cfg) return fail(RL_EINVAL, "problem/cfg is NULL");
@@ -246,7 +258,7 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
     if (prob->N < 0) return fail(RL_EINVAL, "N < 0");
     if ((modes & (RL_MODE_MINCURV | RL_MODE_MINTIME)) == 0 || (modes & ~3)) return fail(RL_EINVAL, "bad modes");
     // any L is accepted like the reference (h = L/N, ref:690); only the pointer is checked
-    if (prob->N > 0 && !prob->center_xy) return fail(RL_EINVAL, "center_xy is NULL");
+    if (prob->N > 0 && !prob->center_xy && !centers) return fail(RL_EINVAL, "center_xy is NULL");
     if (prob->Ei < 0 || prob->Eo < 0 || (prob->Ei > 0 && !prob->inner_seg) || (prob->Eo > 0 && !prob->outer_seg))
         return fail(RL_EINVAL, "bad segments");
     const int mo = cfg[0].max_outer_iters;
@@ -287,13 +299,18 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
     RingHost rh[2] = {make_ring(prob->inner_seg, prob->Ei), make_ring(prob->outer_seg, prob->Eo)};
     const size_t Mt = (size_t)rh[0].M + rh[1].M;
     for (int r = 0; r < 2; ++r) { p->ring_M[r] = rh[r].M; p->ring_dl0[r] = rh[r].dl0; }
-    if ((rc = p->alloc(&p->d_center, 2 * N)) || (rc = p->alloc(&p->d_vtx, 2 * Mt)) ||
+    p->center_stride = centers ? (int64_t)2 * (int64_t)N : 0;
+    if (Ls && (rc = p->alloc(&p->d_Ls, (size_t)B))) return cleanup(rc);
+    if ((rc = p->alloc(&p->d_center, centers ? 2 * N * (size_t)B : 2 * N)) || (rc = p->alloc(&p->d_vtx, 2 * Mt)) ||
         (rc = p->alloc(&p->d_rec, Mt)) || (rc = p->alloc(&p->d_flag, Mt / 32)) ||
         (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
         return cleanup(rc);
     hipStream_t st = p->own_stream;
-    if (p->N > 0 && hipMemcpyAsync(p->d_center, prob->center_xy, 2 * N * sizeof(double), hipMemcpyHostToDevice, st))
+    if (p->N > 0 && hipMemcpyAsync(p->d_center, centers ? centers : prob->center_xy,
+                                   (centers ? (size_t)B : 1) * 2 * N * sizeof(double), hipMemcpyHostToDevice, st))
         return cleanup(fail(RL_EHIP, "upload center"));
+    if (Ls && hipMemcpyAsync(p->d_Ls, Ls, (size_t)B * sizeof(double), hipMemcpyHostToDevice, st))
+        return cleanup(fail(RL_EHIP, "upload L"));
     for (int r = 0, off = 0; r < 2; off += rh[r].M, ++r) {
         const RingHost& R = rh[r];
         if (R.M == 0) continue;
@@ -360,6 +377,8 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         (void)BN;
         rl::KParams kp;
         kp.center = p->d_center;
+        kp.center_stride = p->center_stride;
+        kp.Ls = p->d_Ls;
         for (int r = 0, off = 0; r < 2; off += p->ring_M[r], ++r) {
             kp.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
             kp.ring[r].rec = p->d_rec + off;
@@ -383,6 +402,32 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
     HIPCHK(hipEventRecord(p->ev[3], st));
     p->ran = true;
     return RL_OK;
+}
+
+// B lap evaluations: heading_curv_from_points_generic + velocity_profile_forward_backward
+// with h = L[b]/N on path b (ref:1045-1048, and the debug laps ref:1466-1478) = the
+// min-time driver with max_outer_iters = 0 on per-instance centres.
+int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, int32_t closed, const rl_cfg* cfg,
+                int32_t n_cfg, int32_t device, rl_out* out) {
+    if (!paths_xy || !L || !cfg || !out) return fail(RL_EINVAL, "rl_lap_eval: NULL argument");
+    if (B < 1 || N < 0) return fail(RL_EINVAL, "rl_lap_eval: B < 1 or N < 0");
+    if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
+    std::vector<rl_cfg> c(cfg, cfg + n_cfg);
+    for (auto& x : c) x.max_outer_iters = 0;
+    rl_problem pr{};
+    pr.N = N;
+    pr.closed = closed;
+    pr.L = L[0];
+    rl_plan* p = nullptr;
+    int rc = plan_create_ex(&p, device, &pr, c.data(), n_cfg, nullptr, B, RL_MODE_MINTIME, paths_xy, L);
+    if (rc != RL_OK) return rc;
+    if ((rc = rl_plan_run(p, nullptr)) != RL_OK || (rc = rl_plan_fetch(p, nullptr, out)) != RL_OK) {
+        std::string e = g_err;
+        rl_plan_destroy(p);
+        g_err = e;
+        return rc;
+    }
+    return rl_plan_destroy(p);
 }
 
 // pipeline::compute_geom_and_save rows (ref:1295-1335) on the device

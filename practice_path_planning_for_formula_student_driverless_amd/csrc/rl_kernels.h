@@ -13,7 +13,8 @@ namespace rl {
 // Device pointers of one (problem, mode) launch.  Result/state arrays are
 // instance-major [B][N]; x/y double as the path state P during the run.
 struct KParams {
-    const double* center;      // [N][2]
+    const double* center;      // [N][2], or [B][N][2] with center_stride = 2N (lap evaluation)
+    const double* Ls;          // per-instance L [B] or nullptr (then L)
     RingDesc ring[2];          // inner, outer ring as entry streams (rl_corridor.h)
     const rl_cfg* cfg;         // [ncfg]
     const uint64_t* seeds;     // [B] or nullptr
@@ -22,6 +23,7 @@ struct KParams {
     double *nx, *ny;           // scratch normals [B][N]
     int32_t *evals, *accepts, *sweeps;
     int32_t N, Ei, Eo, ncfg, B, closed;
+    int64_t center_stride;     // doubles between instances' centres (0: shared)
     double L, veh_width;
 };
 

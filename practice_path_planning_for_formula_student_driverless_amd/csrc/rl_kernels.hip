@@ -223,7 +223,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
-    const double h = p.L / (double)N;                    // ref:690 / 913
+    const double Lb = p.Ls ? p.Ls[blockIdx.x] : p.L;
+    const double h = Lb / (double)N;                     // ref:690 / 913
+    const double* __restrict__ CEN = p.center + (size_t)blockIdx.x * (size_t)p.center_stride;
     const double invh = 1.0 / h, inv2h = 1.0 / (2 * h), invh2 = 1.0 / (h * h);   // ref:547, 562
     const double m2invh2 = -2 * invh2;                   // ref:577 (-2*invh2)
     const double two_h = 2 * h, hh = h * h;              // ref:602-603 divisors
@@ -656,8 +658,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (k < cnt) {
-                X[base + k] = p.center[2 * (base + k)];
-                Y[base + k] = p.center[2 * (base + k) + 1];
+                X[base + k] = CEN[2 * (base + k)];
+                Y[base + k] = CEN[2 * (base + k) + 1];
                 ATOT[base + k] = 0.0;
                 ALAST[base + k] = 0.0;
             }

@@ -87,7 +87,9 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
-    const double h = p.L / (double)N;                    // ref:690 / 913
+    const double Lb = p.Ls ? p.Ls[blockIdx.x] : p.L;
+    const double h = Lb / (double)N;                     // ref:690 / 913
+    const double* __restrict__ CEN = p.center + (size_t)blockIdx.x * (size_t)p.center_stride;
     const double invh = 1.0 / h, inv2h = 1.0 / (2 * h), invh2 = 1.0 / (h * h);   // ref:547, 562
     const double m2invh2 = -2 * invh2;
     const double two_h = 2 * h, hh = h * h;
@@ -287,8 +289,8 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
 
     // ---- init ---------------------------------------------------------------
     for (int i = tid; i < N; i += TS) {
-        X[i] = p.center[2 * i];
-        Y[i] = p.center[2 * i + 1];
+        X[i] = CEN[2 * i];
+        Y[i] = CEN[2 * i + 1];
         ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0; GR[i] = 0.0;
     }
     const int MO = C.max_outer_iters;

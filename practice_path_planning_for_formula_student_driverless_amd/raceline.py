@@ -279,15 +279,206 @@ def compute_raceline_and_save(base: str, center_for_opt, s0: float, L: float, cl
 
 
 def compute_mintime_and_save(base: str, center_for_opt, s0: float, L: float, closed: bool, inner_from_mids,
-                             outer_from_mids, cfg: Optional[RlCfg] = None) -> MinTimeResult:
-    """pipeline::compute_mintime_and_save (ref:1385-1438), without the debug dump."""
+                             outer_from_mids, cfg: Optional[RlCfg] = None, debug_dump: bool = True,
+                             device: int = 0) -> MinTimeResult:
+    """pipeline::compute_mintime_and_save (ref:1385-1593).  debug_dump (cfg::debug_dump,
+    on by default in the reference, ref:117) adds the centreline / min-curvature lap
+    evaluations and <base>_debug_compare_paths.csv (debug_dump())."""
+    import sys
     cfg = cfg if cfg is not None else default_cfg()
     res = compute_min_time_raceline(center_for_opt, edges_for(inner_from_mids, closed),
                                     edges_for(outer_from_mids, closed), cfg.veh_width_m, L, closed, cfg)
     write_mintime_csvs(base, res, L, s0=s0)
-    import sys
     sys.stderr.write(f"[mintime] Estimated laptime: {res.lap_time:.3f} s\n")
+    if debug_dump:
+        debug_dump_block(base, center_for_opt, s0, L, closed, res, cfg, device)
     return res
+
+
+# --------------------------------------------------- lap evaluation (§8f row 2)
+def lap_eval(paths, L, closed: bool, cfg: Optional[RlCfg] = None, device: int = 0) -> Outputs:
+    """B lap evaluations on the GPU (rl_lap_eval): heading/curvature with h = L[b]/N and
+    velocity_profile_forward_backward on path b (ref:1045-1048, 1466-1478).
+    paths [B, N, 2]; returns min-time Outputs (heading, kappa, v, ax, lap, sweeps)."""
+    P = np.ascontiguousarray(paths, dtype=np.float64)
+    if P.ndim == 2:
+        P = P[None]
+    B, N = P.shape[0], P.shape[1]
+    Ls = np.ascontiguousarray(np.broadcast_to(np.asarray(L, dtype=np.float64), (B,)))
+    cfg = cfg if cfg is not None else default_cfg()
+    out = Outputs.alloc(B, N, 0, True)         # max_outer_iters = 0: vpass_sweeps [B][1]
+    o = out.as_c()
+    o.evals = None
+    o.accepts = None
+    arr, n = abi.cfg_array(cfg)
+    rc = _lib().rl_lap_eval(abi.dptr(P), abi.dptr(Ls), N, B, 1 if closed else 0, arr, n, int(device), C.byref(o))
+    _check(rc)
+    out.x, out.y = P[:, :, 0].copy(), P[:, :, 1].copy()
+    return out
+
+
+_LIBM = None
+
+
+def _hypot(a: float, b: float) -> float:
+    """glibc hypot (what std::hypot resolves to in the reference build)."""
+    global _LIBM
+    if _LIBM is None:
+        _LIBM = C.CDLL("libm.so.6")
+        _LIBM.hypot.restype = C.c_double
+        _LIBM.hypot.argtypes = [C.c_double, C.c_double]
+    return _LIBM.hypot(a, b)
+
+
+def path_length(P, closed: bool) -> float:
+    """The debug dump's path_length lambda (ref:1443-1448)."""
+    P = np.asarray(P, dtype=np.float64)
+    n = len(P)
+    if n <= 1:
+        return 0.0
+    tot = 0.0
+    for i in range(n - 1):
+        tot += _hypot(P[i + 1, 0] - P[i, 0], P[i + 1, 1] - P[i, 1])
+    if closed and n >= 2:
+        tot += _hypot(P[0, 0] - P[n - 1, 0], P[0, 1] - P[n - 1, 1])
+    return tot
+
+
+def normals_from_points(P, closed: bool) -> np.ndarray:
+    """normals_from_points_generic (ref:581-593) restated on the host."""
+    P = np.asarray(P, dtype=np.float64)
+    N = len(P)
+    n = np.zeros((N, 2))
+    for i in range(N):
+        if N == 1:
+            tx, ty = 1.0, 0.0
+        elif closed:
+            ip, im = (i + 1) % N, (i - 1 + N) % N
+            tx, ty = (P[ip, 0] - P[im, 0]) * 0.5, (P[ip, 1] - P[im, 1]) * 0.5
+        elif i == 0:
+            tx, ty = P[1, 0] - P[0, 0], P[1, 1] - P[0, 1]
+        elif i == N - 1:
+            tx, ty = P[N - 1, 0] - P[N - 2, 0], P[N - 1, 1] - P[N - 2, 1]
+        else:
+            tx, ty = (P[i + 1, 0] - P[i - 1, 0]) * 0.5, (P[i + 1, 1] - P[i - 1, 1]) * 0.5
+        if float(np.sqrt(tx * tx + ty * ty)) < 1e-15:
+            tx, ty = 1.0, 0.0
+        vx, vy = -ty, tx
+        nn = float(np.sqrt(vx * vx + vy * vy))
+        if not (nn < 1e-15):
+            n[i] = (vx / nn, vy / nn)
+    return n
+
+
+DEBUG_HEADER = ("s,cx,cy,mt_x,mt_y,mc_x,mc_y,d_mt_signed_m,d_mc_signed_m,"
+                "d_mt_abs_m,d_mc_abs_m,kappa_mt,v_mt,ax_mt,alat_mt,alat_ratio,"
+                "gamma,a_acc_cap,a_brk_cap,a_power_cap\n")
+
+
+def debug_compare_rows(center, s0: float, L: float, res_mt: "MinTimeResult", mc_path, cfg: RlCfg,
+                       closed: bool) -> np.ndarray:
+    """Rows of <base>_debug_compare_paths.csv (ref:1490-1561), same operations in the
+    same order, libstdc++ min/max/clamp forms."""
+    smax = lambda a, b: b if a < b else a          # noqa: E731  std::max
+    smin = lambda a, b: b if b < a else a          # noqa: E731  std::min
+    nan = float("nan")
+    center = np.asarray(center, dtype=np.float64)
+    Pmt = np.asarray(res_mt.raceline, dtype=np.float64)
+    mc = np.asarray(mc_path, dtype=np.float64).reshape(-1, 2) if mc_path is not None else np.zeros((0, 2))
+    nc = normals_from_points(center, closed)
+    N = min(len(Pmt), len(center))
+    rows = np.zeros((N, 20))
+    c = cfg
+    for k in range(N):
+        si = s0 + L * (float(k) / float(max(1, N)))
+        cx, cy = center[k]
+        mx, my = Pmt[k]
+        if len(mc) > k:
+            ccx, ccy = mc[k]
+        else:
+            ccx = ccy = nan
+        dmt = (mx - cx) * nc[k, 0] + (my - cy) * nc[k, 1]
+        dmc = (ccx - cx) * nc[k, 0] + (ccy - cy) * nc[k, 1] if np.isfinite(ccx) else nan
+        admt = abs(dmt)
+        admc = abs(dmc) if np.isfinite(dmc) else nan
+        kap = float(res_mt.curvature[k]) if k < len(res_mt.curvature) else 0.0
+        v = float(res_mt.v[k]) if k < len(res_mt.v) else 0.0
+        ax = float(res_mt.ax[k]) if k < len(res_mt.ax) else 0.0
+        alat = v * v * abs(kap)
+        alat_ratio = smin(1.0, alat / c.a_total_max) if c.a_total_max > 1e-9 else 0.0
+        vkappa = float(np.sqrt(c.a_lat_max / smax(abs(kap), c.kappa_eps)))
+        x = (vkappa - v) / smax(1e-6, vkappa)
+        pen = 0.0 if x < 0 else (1.0 if x > 1 else x)
+        gamma = 1.0 + c.w_time_gain * pen
+        alatloc = v * v * abs(kap)
+        a_res = float(np.sqrt(smax(0.0, c.a_total_max * c.a_total_max - alatloc * alatloc)))
+        Fd = 0.5 * c.rho_air * c.Cd * c.A_front_m2 * v * v
+        Fr = c.mass_kg * 9.81 * c.c_rr
+        a_power = (c.P_max_W / (c.mass_kg * v) - (Fd + Fr) / c.mass_kg) if (c.P_max_W > 0 and v > 1e-6) else 1e9
+        m3 = a_res                                     # std::min({a_res, acc_cap, a_power})
+        if c.a_long_acc_cap < m3:
+            m3 = c.a_long_acc_cap
+        if a_power < m3:
+            m3 = a_power
+        a_acc = smax(0.0, m3)
+        a_brk = smax(0.0, smin(a_res, c.a_long_brake_cap) + (Fd + Fr) / c.mass_kg)
+        a_pow = smax(0.0, a_power)
+        rows[k] = (si - s0, cx, cy, mx, my, ccx, ccy, dmt, dmc, admt, admc, kap, v, ax, alat, alat_ratio,
+                   gamma, a_acc, a_brk, a_pow)
+    return rows
+
+
+def format_debug_compare_csv(rows: np.ndarray) -> str:
+    out = [DEBUG_HEADER]
+    for r in np.asarray(rows, dtype=np.float64).reshape(-1, 20):
+        out.append(",".join(_f9(v) for v in r) + "\n")
+    return "".join(out)
+
+
+def debug_dump_block(base: str, center_for_opt, s0: float, L: float, closed: bool, res_mt: "MinTimeResult",
+               cfg: RlCfg, device: int = 0, debug_offset_warn_m: float = 0.04, log=None) -> dict:
+    """The cfg::debug_dump block of compute_mintime_and_save (ref:1441-1593): centreline
+    and min-curvature laps with the same dynamics (two GPU lap evaluations), and
+    <base>_debug_compare_paths.csv.  The min-curvature path is re-read from
+    <base>_raceline.csv as the reference does (ref:1452-1459)."""
+    import sys
+    log = log if log is not None else sys.stderr
+    center = np.asarray(center_for_opt, dtype=np.float64).reshape(-1, 2)
+    mc = load_csv_xy(base + "_raceline.csv") if os.path.exists(base + "_raceline.csv") else np.zeros((0, 2))
+    if len(mc) and closed and len(mc) >= 2 and abs(mc[0, 0] - mc[-1, 0]) <= 1e-12 and abs(mc[0, 1] - mc[-1, 1]) <= 1e-12:
+        mc = mc[:-1]
+    Nc = len(center)
+    laps = {}
+    if Nc:
+        paths, Ls = [center], [L]
+        if len(mc) == Nc:
+            paths.append(mc)
+            Ls.append(path_length(mc, closed))
+        ev = lap_eval(np.stack(paths), np.array(Ls), closed, cfg, device)
+        laps["center"] = float(ev.lap[0])
+        if len(paths) == 2:
+            laps["mincurv"] = float(ev.lap[1])
+        elif len(mc):
+            laps["mincurv"] = float(lap_eval(mc, [path_length(mc, closed)], closed, cfg, device).lap[0])
+    lap_c = laps.get("center", 0.0)
+    if "mincurv" in laps:
+        log.write(f"[debug] centerline lap ≈ {lap_c:.3f} s,  min-curv lap ≈ {laps['mincurv']:.3f} s,  "
+                  f"min-time lap ≈ {res_mt.lap_time:.3f} s\n")
+    else:
+        log.write(f"[debug] centerline lap ≈ {lap_c:.3f} s,  (min-curv not found),  min-time lap ≈ {res_mt.lap_time:.3f} s\n")
+    rows = debug_compare_rows(center, s0, L, res_mt, mc if len(mc) else None, cfg, closed)
+    with open(base + "_debug_compare_paths.csv", "w") as f:
+        f.write(format_debug_compare_csv(rows))
+    N = len(rows)
+    admt, admc = rows[:, 9], rows[:, 10]
+    stats = {"laps": laps, "mean_abs_mt": float(np.sum(admt) / max(1, N)) if N else 0.0,
+             "max_abs_mt": float(np.max(admt)) if N else 0.0,
+             "near_cnt": int(np.sum(admt < debug_offset_warn_m))}
+    log.write(f"[debug] min-time vs center: mean|offset|={stats['mean_abs_mt']:.3f} m, "
+              f"max={stats['max_abs_mt']:.3f} m, within {debug_offset_warn_m:.3f} m : {stats['near_cnt']}/{N}\n")
+    if "mincurv" in laps and laps["mincurv"] > 0:
+        log.write(f"[debug] lap gain vs min-curv: {(laps['mincurv'] - res_mt.lap_time) / laps['mincurv'] * 100.0:.3f} %\n")
+    return stats
 
 
 # ------------------------------------------------------- step 6: geometry

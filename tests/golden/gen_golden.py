@@ -171,7 +171,73 @@ def geom_fixtures(ref, manifest):
         print("geom", tag, d["rows"].shape, d["knots"].shape)
 
 
+def debug_fixtures(ref, manifest):
+    """SURVEY §8f row 2: the reference CLI with cfg::debug_dump on (its default): its own
+    <base>_debug_compare_paths.csv and <base>_raceline.csv, and the two debug laps
+    (centreline with h = L/N, min-curvature path re-read from the CSV with h = polyline
+    length / N; main.cpp:1452-1478) at full precision from the reference's functions."""
+    csv_dir = os.path.join(HERE, "ref_csv")
+    manifest["debug_cases"] = {}
+    for tag, tr, closed, track_case in (("training_map", "training_map", True, "track_training_map"),
+                                        ("competition_map2", "competition_map2", True, "track_competition_map2"),
+                                        ("training_open", "training_map", False, "training_open")):
+        ref.reset()
+        ref.lib.ref_set_closed(1 if closed else 0)
+        ref.lib.ref_set_debug(1)
+        d = os.path.join(ref.tmp, "dbg_" + tag)
+        os.makedirs(d)
+        base = os.path.join(d, "t_centerline")
+        rc = ref.lib.ref_run_cli(f"{REF_CSV}/{tr}_inner.csv".encode(), f"{REF_CSV}/{tr}_outer.csv".encode(),
+                                 (base + ".csv").encode())
+        assert rc == 0, rc
+        shutil.copy(base + "_debug_compare_paths.csv", os.path.join(csv_dir, f"debug_{tag}_compare_paths.csv"))
+        shutil.copy(base + "_raceline.csv", os.path.join(csv_dir, f"debug_{tag}_raceline.csv"))
+        with np.load(os.path.join(HERE, manifest["cases"][track_case]["file"]), allow_pickle=False) as z:
+            center, L = z["center"], float(z["L"])
+        mc = []
+        for line in open(base + "_raceline.csv"):
+            if line.strip():
+                x, y = line.replace(",", " ").split()[:2]
+                mc.append((float(x), float(y)))
+        mc = np.array(mc)
+        if closed and len(mc) >= 2 and abs(mc[0, 0] - mc[-1, 0]) <= 1e-12 and abs(mc[0, 1] - mc[-1, 1]) <= 1e-12:
+            mc = mc[:-1]
+        libm = C.CDLL("libm.so.6")          # std::hypot in the reference build = glibc hypot
+        libm.hypot.restype = C.c_double
+        libm.hypot.argtypes = [C.c_double, C.c_double]
+        laps = {}
+        for name, P, Lp in (("center", center, L), ("mincurv", mc, None)):
+            P = np.ascontiguousarray(P, dtype=np.float64)
+            N = len(P)
+            if Lp is None:   # path_length (main.cpp:1443-1448), serial glibc hypot sums
+                Lp = 0.0
+                for i in range(N - 1):
+                    Lp += libm.hypot(P[i + 1, 0] - P[i, 0], P[i + 1, 1] - P[i, 1])
+                if closed:
+                    Lp += libm.hypot(P[0, 0] - P[N - 1, 0], P[0, 1] - P[N - 1, 1])
+            h = Lp / max(1, N)
+            arr = [np.zeros(N) for _ in range(4)]
+            lap = C.c_double()
+            ref.lib.ref_lap_eval(vp(P), N, C.c_double(h), 1 if closed else 0, *[vp(a) for a in arr], C.byref(lap))
+            laps[name] = {"L": Lp, "h": h, "lap": lap.value}
+            np.savez_compressed(os.path.join(HERE, f"debug_{tag}_{name}.npz"), path=P, heading=arr[0], kappa=arr[1],
+                                v=arr[2], ax=arr[3], lap=np.float64(lap.value), L=np.float64(Lp))
+        manifest["debug_cases"][tag] = {"track_case": track_case, "closed": closed, "laps": laps,
+                                        "compare_csv": f"ref_csv/debug_{tag}_compare_paths.csv",
+                                        "raceline_csv": f"ref_csv/debug_{tag}_raceline.csv"}
+        print("debug", tag, laps)
+
+
 def main():
+    if "--debug" in sys.argv:
+        ref = Ref()
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        debug_fixtures(ref, manifest)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        shutil.rmtree(ref.tmp, ignore_errors=True)
+        return
     if "--geom" in sys.argv:
         ref = Ref()
         with open(os.path.join(HERE, "manifest.json")) as f:
@@ -285,6 +351,7 @@ def main():
         shutil.copy(os.path.join(cli_dir, "training_map_centerline" + suffix), os.path.join(csv_dir, "training_map" + suffix))
     manifest["ref_csv"] = {"track": "training_map", "dir": "ref_csv"}
     geom_fixtures(ref, manifest)
+    debug_fixtures(ref, manifest)
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

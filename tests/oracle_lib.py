@@ -143,3 +143,26 @@ def run_oracle_geom(gp: abi.GeomProblem, cfg: abi.RlCfg) -> np.ndarray:
     n = oracle().oracle_geom(C.byref(g), C.byref(cfg), rows.ctypes.data_as(C.POINTER(C.c_double)))
     assert n == gp.rows, n
     return rows[: gp.rows]
+
+
+# ------------------------------------------------- debug dump / lap evaluation
+def load_debug_case(tag: str) -> dict:
+    meta = manifest()["debug_cases"][tag]
+    out = {"_meta": meta}
+    for name in ("center", "mincurv"):
+        with np.load(os.path.join(GOLDEN, f"debug_{tag}_{name}.npz"), allow_pickle=False) as z:
+            out[name] = {k: z[k] for k in z.files}
+    for key in ("compare_csv", "raceline_csv"):
+        with open(os.path.join(GOLDEN, meta[key]), "rb") as f:
+            out[key] = f.read()
+    out["track"] = load_case(meta["track_case"])
+    return out
+
+
+def run_oracle_lap_eval(path: np.ndarray, L: float, closed: bool, cfg: abi.RlCfg):
+    """The oracle's min-time driver with max_outer_iters = 0 = heading/kappa + v-pass
+    with h = L/N (ref:1045-1048)."""
+    c = abi.RlCfg.from_dict(cfg.to_dict())
+    c.max_outer_iters = 0
+    prob = abi.Problem(center=path, L=L, inner_seg=np.zeros((0, 4)), outer_seg=np.zeros((0, 4)), closed=closed)
+    return run_oracle(prob, c, B=1, modes=(False, True))[1]

@@ -3,6 +3,8 @@ fixtures and the CPU oracle.  Tolerance (BASELINE.json
 north_star): per column |gpu-ref| <= 1e-4*max|ref| + 1e-9; lap |Δ|/lap <= 1e-4.
 Integer outputs (evals/accepts per outer, v-pass sweeps) must match the oracle.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -358,6 +360,54 @@ def test_geom_segment_lists_and_edges():
         np.testing.assert_array_equal(rows[:, 5:8], orc[:, 5:8])
         for j in range(9):
             col_close(rows[:, j], orc[:, j], f"geom.K{K}.{j}")
+
+
+DEBUG = list(O.manifest().get("debug_cases", {}))
+
+
+@pytest.mark.parametrize("tag", DEBUG)
+def test_lap_eval_vs_reference(tag):
+    """rl_lap_eval: the centreline and min-curvature laps of the debug
+    dump in one batch, vs the reference's full-precision lap evaluations."""
+    _lib_or_skip()
+    d = O.load_debug_case(tag)
+    closed = d["_meta"]["closed"]
+    cfg = O.case_cfg(d["track"])
+    c, m = d["center"], d["mincurv"]
+    if len(c["path"]) == len(m["path"]):
+        ev = raceline.lap_eval(np.stack([c["path"], m["path"]]), [float(c["L"]), float(m["L"])], closed, cfg)
+        got = {"center": 0, "mincurv": 1}
+    else:
+        ev = None
+    for name, f in (("center", c), ("mincurv", m)):
+        if ev is not None:
+            b, e = got[name], ev
+        else:
+            b, e = 0, raceline.lap_eval(f["path"], [float(f["L"])], closed, cfg)
+        assert abs(e.lap[b] - float(f["lap"])) / float(f["lap"]) <= REL
+        for k in ("kappa", "v", "ax", "heading"):
+            col_close(getattr(e, k)[b], f[k], f"lap_eval.{tag}.{name}.{k}")
+        orc = O.run_oracle_lap_eval(f["path"], float(f["L"]), closed, cfg)
+        np.testing.assert_array_equal(e.vpass_sweeps[b], orc.vpass_sweeps[0][:1])
+
+
+def test_pipeline_csvs_match_reference_cli(tmp_path):
+    """The GPU pipeline (compute_raceline_and_save + compute_mintime_and_save with the
+    debug dump) writes the reference CLI's CSV files for training_map byte for byte."""
+    _lib_or_skip()
+    d = O.load_debug_case("training_map")
+    track = d["track"]
+    base = str(tmp_path / "t_centerline")
+    cfg = O.case_cfg(track)
+    center, s0, L = track["center"], float(track["s0"]), float(track["L"])
+    raceline.compute_raceline_and_save(base, center, s0, L, True, track["inner_ring"], track["outer_ring"], cfg)
+    raceline.compute_mintime_and_save(base, center, s0, L, True, track["inner_ring"], track["outer_ring"], cfg)
+    assert open(base + "_raceline.csv", "rb").read() == d["raceline_csv"]
+    assert open(base + "_debug_compare_paths.csv", "rb").read() == d["compare_csv"]
+    man = O.manifest()["ref_csv"]
+    for suffix in ("_raceline_with_geom.csv", "_mintime_raceline.csv", "_mintime_with_geom.csv"):
+        ref = open(os.path.join(O.GOLDEN, man["dir"], man["track"] + suffix), "rb").read()
+        assert open(base + suffix, "rb").read() == ref, suffix
 
 
 def test_errors_fail_loudly():
