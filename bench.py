@@ -216,6 +216,32 @@ def run_step6(world, rank):
             "csv_bytes_equal_reference": raceline.format_geom_csv(rows).encode() == case["_csv"]}
 
 
+def run_lapeval(world, rank, racelines):
+    """batched lap evaluations (heading/kappa + v-pass, h = L/N) of the
+    C2 run's 1024 optimised racelines (rank 0's), GPU vs the CPU oracle on a sample."""
+    import oracle_lib as O
+
+    if rank != 0:
+        return None
+    case, prob, cfg = load_problem("cmap1_n2000")
+    P = np.ascontiguousarray(racelines)
+    B, N = P.shape[0], P.shape[1]
+    Ls = np.full(B, float(prob.L))
+    raceline.lap_eval(P[:8], Ls[:8], True, cfg)                        # warm-up
+    t0 = time.perf_counter()
+    ev, kms = raceline.lap_eval(P, Ls, True, cfg, return_ms=True)
+    wall = time.perf_counter() - t0
+    n_cpu, t0 = 0, time.perf_counter()
+    while n_cpu < B and time.perf_counter() - t0 < 3.0:
+        orc = O.run_oracle_lap_eval(P[n_cpu], float(prob.L), True, cfg)
+        assert abs(orc.lap[0] - ev.lap[n_cpu]) <= 1e-9 * orc.lap[0]
+        n_cpu += 1
+    cpu_s = (time.perf_counter() - t0) / n_cpu
+    return {"paths": B, "N": N, "kernel_ms": round(kms, 3), "wall_ms_incl_transfers": round(1e3 * wall, 2),
+            "laps_per_s_kernel": round(B / (kms * 1e-3), 1), "cpu_oracle_laps_per_s_1core": round(1.0 / cpu_s, 1),
+            "cpu_sample": f"{n_cpu} paths", "lap_min_s": float(ev.lap.min()), "lap_max_s": float(ev.lap.max())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -312,6 +338,7 @@ def main():
 
     c4 = None if args.no_extras else run_c4(world, rank, local, dev, dist)
     st6 = None if args.no_extras else run_step6(world, rank)
+    lev = None if args.no_extras else run_lapeval(world, rank, np.stack([res["x"].cpu().numpy(), res["y"].cpu().numpy()], axis=2))
     c5 = None if args.no_extras else run_c5(world, rank, local, dev, dist)
     if rank != 0:
         plan.close()
@@ -392,6 +419,8 @@ def main():
         extras["c5_oval_n10000"] = c5
     if st6 is not None:
         extras["step6_geom_cmap1_n2000"] = st6
+    if lev is not None:
+        extras["lap_eval_1024_racelines_n2000"] = lev
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(prob, cfg)

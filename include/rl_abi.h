@@ -191,9 +191,10 @@ int rl_plan_destroy(rl_plan* plan);
  * (ref:1045-1048) and the debug dump's centreline / min-curvature laps (ref:1466-1478),
  * i.e. compute_min_time_raceline with max_outer_iters = 0.  paths_xy [B][N][2], L [B];
  * `out` receives heading, kappa, v, ax, lap and vpass_sweeps [B][1] (x, y echo the path,
- * alphas are 0); evals/accepts may be NULL.  cfg[n_cfg] as in rl_optimize. */
+ * alphas are 0); evals/accepts may be NULL.  cfg[n_cfg] as in rl_optimize.
+ * *kernel_ms (optional): HIP-event time of the kernel. */
 int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, int32_t closed,
-                const rl_cfg* cfg, int32_t n_cfg, int32_t device, rl_out* out);
+                const rl_cfg* cfg, int32_t n_cfg, int32_t device, rl_out* out, float* kernel_ms);
 
 /* ------------------------------------------------------- step 6: geometry
  * pipeline::compute_geom_and_save (ref:1295-1335), the rows of <base>_with_geom.csv:

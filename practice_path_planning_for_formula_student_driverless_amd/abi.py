@@ -365,7 +365,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                             C.POINTER(C.c_float)]
     lib.rl_geom.restype = C.c_int
     lib.rl_lap_eval.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32, C.c_int32, C.c_int32,
-                                C.POINTER(RlCfg), C.c_int32, C.c_int32, C.POINTER(RlOut)]
+                                C.POINTER(RlCfg), C.c_int32, C.c_int32, C.POINTER(RlOut), C.POINTER(C.c_float)]
     lib.rl_lap_eval.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib

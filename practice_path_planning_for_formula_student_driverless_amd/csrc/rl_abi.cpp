@@ -408,7 +408,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
 // with h = L[b]/N on path b (ref:1045-1048, and the debug laps ref:1466-1478) = the
 // min-time driver with max_outer_iters = 0 on per-instance centres.
 int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, int32_t closed, const rl_cfg* cfg,
-                int32_t n_cfg, int32_t device, rl_out* out) {
+                int32_t n_cfg, int32_t device, rl_out* out, float* kernel_ms) {
     if (!paths_xy || !L || !cfg || !out) return fail(RL_EINVAL, "rl_lap_eval: NULL argument");
     if (B < 1 || N < 0) return fail(RL_EINVAL, "rl_lap_eval: B < 1 or N < 0");
     if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
@@ -421,7 +421,8 @@ int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, i
     rl_plan* p = nullptr;
     int rc = plan_create_ex(&p, device, &pr, c.data(), n_cfg, nullptr, B, RL_MODE_MINTIME, paths_xy, L);
     if (rc != RL_OK) return rc;
-    if ((rc = rl_plan_run(p, nullptr)) != RL_OK || (rc = rl_plan_fetch(p, nullptr, out)) != RL_OK) {
+    if ((rc = rl_plan_run(p, nullptr)) != RL_OK || (rc = rl_plan_fetch(p, nullptr, out)) != RL_OK ||
+        (kernel_ms && (rc = rl_plan_kernel_ms(p, 2, kernel_ms)) != RL_OK)) {
         std::string e = g_err;
         rl_plan_destroy(p);
         g_err = e;

@@ -296,7 +296,7 @@ def compute_mintime_and_save(base: str, center_for_opt, s0: float, L: float, clo
 
 
 # --------------------------------------------------- lap evaluation (§8f row 2)
-def lap_eval(paths, L, closed: bool, cfg: Optional[RlCfg] = None, device: int = 0) -> Outputs:
+def lap_eval(paths, L, closed: bool, cfg: Optional[RlCfg] = None, device: int = 0, return_ms: bool = False):
     """B lap evaluations on the GPU (rl_lap_eval): heading/curvature with h = L[b]/N and
     velocity_profile_forward_backward on path b (ref:1045-1048, 1466-1478).
     paths [B, N, 2]; returns min-time Outputs (heading, kappa, v, ax, lap, sweeps)."""
@@ -311,10 +311,12 @@ def lap_eval(paths, L, closed: bool, cfg: Optional[RlCfg] = None, device: int = 
     o.evals = None
     o.accepts = None
     arr, n = abi.cfg_array(cfg)
-    rc = _lib().rl_lap_eval(abi.dptr(P), abi.dptr(Ls), N, B, 1 if closed else 0, arr, n, int(device), C.byref(o))
+    ms = C.c_float(0.0)
+    rc = _lib().rl_lap_eval(abi.dptr(P), abi.dptr(Ls), N, B, 1 if closed else 0, arr, n, int(device), C.byref(o),
+                            C.byref(ms))
     _check(rc)
     out.x, out.y = P[:, :, 0].copy(), P[:, :, 1].copy()
-    return out
+    return (out, float(ms.value)) if return_ms else out
 
 
 _LIBM = None
