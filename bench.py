@@ -242,6 +242,39 @@ def run_lapeval(world, rank, racelines):
             "cpu_sample": f"{n_cpu} paths", "lap_min_s": float(ev.lap.min()), "lap_max_s": float(ev.lap.max())}
 
 
+def run_format(world, rank, mc_x, mc_y, mc_k, mc_al, case, cfg):
+    """the _raceline_with_geom.csv tables (7 columns, N+1 rows) of the
+    C2 run's 1024 instances formatted on the GPU in one pass (rl_format_csv), vs glibc
+    "%.9f" on one core over a sample (the oracle's snprintf loop)."""
+    import oracle_lib as O
+
+    if rank != 0:
+        return None
+    B, N = mc_x.shape
+    L, s0 = float(case["L"]) if "L" in case else 0.0, float(case["s0"]) if "s0" in case else 0.0
+    s = (s0 + L * (np.arange(N) / float(N))) - s0
+    T = np.zeros((B, N + 1, 7))
+    T[:, :N, 0] = s
+    T[:, :N, 1], T[:, :N, 2], T[:, :N, 4], T[:, :N, 5] = mc_x, mc_y, mc_k, mc_al
+    T[:, :N, 3] = np.arctan2(np.gradient(mc_y, axis=1), np.gradient(mc_x, axis=1))     # a heading-like column
+    T[:, :N, 6] = np.minimum(cfg.v_cap_mps, np.sqrt(cfg.a_lat_max / np.maximum(np.abs(mc_k), cfg.kappa_eps)))
+    T[:, N] = T[:, 0]
+    T[:, N, 0] = L
+    T = T.reshape(-1, 7)
+    raceline.format_table(T[:100])                                      # warm-up
+    t0 = time.perf_counter()
+    text = raceline.format_table(T)
+    gpu_s = time.perf_counter() - t0
+    k = max(1, min(T.shape[0], 200000))
+    t0 = time.perf_counter()
+    cpu_text = O.oracle_format_rows(T[:k])
+    cpu_s = time.perf_counter() - t0
+    return {"rows": int(T.shape[0]), "numbers": int(T.size), "bytes": len(text),
+            "gpu_wall_ms_incl_transfers": round(1e3 * gpu_s, 2), "gpu_MB_per_s": round(len(text) / gpu_s / 1e6, 1),
+            "cpu_glibc_MB_per_s_1core": round(len(cpu_text) / cpu_s / 1e6, 1), "cpu_sample_rows": k,
+            "bytes_equal_on_sample": text[: len(cpu_text)] == cpu_text}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -339,6 +372,8 @@ def main():
     c4 = None if args.no_extras else run_c4(world, rank, local, dev, dist)
     st6 = None if args.no_extras else run_step6(world, rank)
     lev = None if args.no_extras else run_lapeval(world, rank, np.stack([res["x"].cpu().numpy(), res["y"].cpu().numpy()], axis=2))
+    fmt = None if args.no_extras else run_format(world, rank, res["x"].cpu().numpy(), res["y"].cpu().numpy(),
+                                                   res["kappa"].cpu().numpy(), res["alpha_last"].cpu().numpy(), case, cfg)
     c5 = None if args.no_extras else run_c5(world, rank, local, dev, dist)
     if rank != 0:
         plan.close()
@@ -421,6 +456,8 @@ def main():
         extras["step6_geom_cmap1_n2000"] = st6
     if lev is not None:
         extras["lap_eval_1024_racelines_n2000"] = lev
+    if fmt is not None:
+        extras["csv_format_1024_instances"] = fmt
     cpu = None
     if world == 1 and not args.no_cpu:
         cpu = cpu_baseline(prob, cfg)

@@ -233,6 +233,17 @@ typedef struct rl_geom_problem {
  * count or RL_E*. */
 int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double* rows, float* kernel_ms);
 
+/* ------------------------------------------------------ CSV number format
+ * SURVEY §8f row 3.  The reference writes every CSV with std::fixed + precision(9)
+ * (ref:1284, 1303, 1354, 1418, 1495), i.e. glibc "%.9f": exact value rounded to 9
+ * fraction digits with ties to even, "-" whenever the sign bit is set, "nan"/"-nan",
+ * "inf"/"-inf".  rl_format_csv formats a row-major table [rows][cols] on the GPU into
+ * `out` as "v,v,...,v\n" rows (no header).  *out_len receives the byte count (also when
+ * out_cap is too small: then RL_ETOOBIG); row_offsets [rows+1] (optional) the start of
+ * every row.  Values with |x| >= 9.2e9 are rejected (RL_ETOOBIG). */
+int rl_format_csv(const double* table, int64_t rows, int32_t cols, int32_t device, char* out, int64_t out_cap,
+                  int64_t* out_len, int64_t* row_offsets);
+
 /* ------------------------------------------------------------- runtime */
 int         rl_device_count(void);
 const char* rl_last_error(void);

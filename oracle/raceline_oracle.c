@@ -21,6 +21,7 @@
  * alpha seeds of SURVEY.md §8d (seed 0 == the reference exactly).
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -581,6 +582,23 @@ int oracle_geom(const rl_geom_problem* gp, const rl_cfg* C, double* rows) {
         r[0] = gp->L;
     }
     return Kmax + (gp->emit_closed_duplicate ? 1 : 0);
+}
+
+/* CSV rows of a [rows][cols] table with glibc "%.9f" (what std::fixed/precision(9)
+ * produces, ref:1303) — the CPU side of the formatter benchmark and checker.
+ * Returns the byte count, or -1 if cap is too small. */
+long long oracle_format_rows(const double* t, long long rows, int cols, char* out, long long cap) {
+    long long n = 0;
+    char tmp[64];
+    for (long long r = 0; r < rows; ++r)
+        for (int c = 0; c < cols; ++c) {
+            int k = snprintf(tmp, sizeof tmp, "%.9f", t[r * cols + c]);
+            if (n + k + 1 > cap) return -1;
+            memcpy(out + n, tmp, (size_t)k);
+            n += k;
+            out[n++] = (c + 1 < cols) ? ',' : '\n';
+        }
+    return n;
 }
 
 /* edges::ringEdges ref:251-255 / polylineEdges ref:256-260 */

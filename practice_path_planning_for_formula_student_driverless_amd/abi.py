@@ -367,6 +367,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_lap_eval.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32, C.c_int32, C.c_int32,
                                 C.POINTER(RlCfg), C.c_int32, C.c_int32, C.POINTER(RlOut), C.POINTER(C.c_float)]
     lib.rl_lap_eval.restype = C.c_int
+    lib.rl_format_csv.argtypes = [C.POINTER(C.c_double), C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int64,
+                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    lib.rl_format_csv.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib
     return lib

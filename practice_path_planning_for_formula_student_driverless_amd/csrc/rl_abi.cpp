@@ -533,6 +533,52 @@ int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double
     return finish(nrows);
 }
 
+// glibc "%.9f" CSV rows of a host table, formatted on the device (rl_format.hip)
+int rl_format_csv(const double* table, int64_t rows, int32_t cols, int32_t device, char* out, int64_t out_cap,
+                  int64_t* out_len, int64_t* row_offsets) {
+    if (!out_len || rows < 0 || cols < 1 || (rows > 0 && !table) || (out_cap > 0 && !out))
+        return fail(RL_EINVAL, "rl_format_csv: bad argument");
+    *out_len = 0;
+    if (rows == 0) {
+        if (row_offsets) row_offsets[0] = 0;
+        return RL_OK;
+    }
+    if (rows > (int64_t)1 << 31) return fail(RL_ETOOBIG, "rl_format_csv: more than 2^31 rows");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    const uint64_t cap = (uint64_t)rows * (uint64_t)cols * 22;
+    double* d_tab = nullptr;
+    char* d_out = nullptr;
+    uint64_t* d_offs = nullptr;
+    hipStream_t st = nullptr;
+    auto done = [&](int code) {
+        if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
+        if (d_tab) hipFree(d_tab);
+        if (d_out) hipFree(d_out);
+        if (d_offs) hipFree(d_offs);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return done(fail(RL_EHIP, "stream"));
+    if (hipMalloc((void**)&d_tab, (size_t)rows * cols * 8) != hipSuccess || hipMalloc((void**)&d_out, cap) != hipSuccess ||
+        hipMalloc((void**)&d_offs, (size_t)(rows + 1) * 8) != hipSuccess)
+        return done(fail(RL_ENOMEM, "rl_format_csv: hipMalloc failed"));
+    if (hipMemcpyAsync(d_tab, table, (size_t)rows * cols * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+        return done(fail(RL_EHIP, "rl_format_csv: upload"));
+    uint64_t total = 0;
+    const int rc = rl::format_rows(d_tab, rows, cols, d_out, cap, d_offs, &total, st);
+    if (rc == -1) return done(fail(RL_ETOOBIG, "rl_format_csv: a value with |x| >= 9.2e9"));
+    if (rc != 0) return done(fail(RL_EHIP, "rl_format_csv: device formatting failed"));
+    *out_len = (int64_t)total;
+    if ((int64_t)total > out_cap) return done(fail(RL_ETOOBIG, "rl_format_csv: out_cap too small (see *out_len)"));
+    if (hipMemcpyAsync(out, d_out, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (row_offsets && hipMemcpyAsync(row_offsets, d_offs, (size_t)(rows + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return done(fail(RL_EHIP, "rl_format_csv: download"));
+    return done(RL_OK);
+}
+
 int rl_plan_kernel_ms(rl_plan* p, int32_t idx, float* ms) {
     if (!p || !ms || !p->ran) return fail(RL_EINVAL, "plan not run");
     HIPCHK(hipSetDevice(p->device));

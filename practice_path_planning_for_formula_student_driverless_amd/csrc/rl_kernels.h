@@ -53,6 +53,10 @@ struct GeomParams {
     double* rows;
 };
 hipError_t launch_geom(const GeomParams& g, hipStream_t st);
+// "%.9f" CSV rows of a [rows][cols] device table (rl_format.hip): 0, -1 (|x| >= 9.2e9),
+// -2 (cap short; *total = needed), -3 (HIP failure)
+int format_rows(const double* table, int64_t rows, int cols, char* out, uint64_t cap, uint64_t* offs,
+                uint64_t* total, hipStream_t st);
 #ifdef RL_STAMPS
 int debug_stamps(unsigned long long* host, int nblocks);
 #endif

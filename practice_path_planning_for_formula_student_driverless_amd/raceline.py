@@ -521,6 +521,46 @@ def compute_geom_and_save(base: str, gp: GeomProblem, cfg: Optional[RlCfg] = Non
     return rows
 
 
+# ------------------------------------------------- CSV number format (§8f row 3)
+def format_table(table, device: int = 0, return_offsets: bool = False):
+    """glibc "%.9f" CSV rows ("v,...,v\\n") of a [rows, cols] table, formatted on the GPU
+    (rl_format_csv); byte-identical to the reference's std::fixed/precision(9) output."""
+    T = np.ascontiguousarray(table, dtype=np.float64)
+    if T.ndim == 1:
+        T = T[:, None]
+    rows, cols = T.shape
+    cap = rows * cols * 22
+    buf = C.create_string_buffer(max(cap, 1))
+    n = C.c_int64(0)
+    offs = np.zeros(rows + 1, dtype=np.int64)
+    rc = _lib().rl_format_csv(abi.dptr(T), rows, cols, int(device), C.cast(buf, C.c_void_p), cap, C.byref(n),
+                              offs.ctypes.data_as(C.POINTER(C.c_int64)))
+    _check(rc)
+    text = buf.raw[: n.value]
+    return (text, offs) if return_offsets else text
+
+
+def write_batch_raceline_with_geom(bases, mc: Outputs, L: float, cfg: Optional[RlCfg] = None, s0: float = 0.0,
+                                   emit_closed_duplicate: bool = True, device: int = 0) -> None:
+    """<base_b>_raceline_with_geom.csv (ref:1362-1381) for all B instances of a batch in
+    one GPU formatting pass (rows split by the returned offsets)."""
+    cfg = cfg if cfg is not None else default_cfg()
+    B, N = mc.x.shape
+    s = np.array([_s_rel(s0, L, k, N) for k in range(N)])
+    vk = lambda kap: np.array([_vkappa(k, cfg) for k in kap])          # noqa: E731
+    per = N + (1 if (emit_closed_duplicate and N) else 0)
+    T = np.zeros((B, per, 7))
+    for b in range(B):
+        T[b, :N] = np.stack([s, mc.x[b], mc.y[b], mc.heading[b], mc.kappa[b], mc.alpha_last[b], vk(mc.kappa[b])], 1)
+        if per > N:
+            T[b, N] = (L, *T[b, 0, 1:])
+    text, offs = format_table(T.reshape(B * per, 7), device, return_offsets=True)
+    head = b"s,x,y,heading_rad,curvature,alpha_last,v_kappa_mps\n"
+    for b, base in enumerate(bases):
+        with open(base + "_raceline_with_geom.csv", "wb") as f:
+            f.write(head + text[offs[b * per]: offs[(b + 1) * per]])
+
+
 def load_csv_xy(path: str) -> np.ndarray:
     """io::loadCSV_XY (ref:267-279): x,y per line; ',' ';' tab or space."""
     pts = []

@@ -47,6 +47,8 @@ def oracle() -> C.CDLL:
         lib.oracle_ring_segments.restype = C.c_int
         lib.oracle_geom.argtypes = [C.POINTER(abi.RlGeomProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double)]
         lib.oracle_geom.restype = C.c_int
+        lib.oracle_format_rows.argtypes = [C.POINTER(C.c_double), C.c_longlong, C.c_int, C.c_char_p, C.c_longlong]
+        lib.oracle_format_rows.restype = C.c_longlong
         _ORACLE = lib
     return _ORACLE
 
@@ -166,3 +168,13 @@ def run_oracle_lap_eval(path: np.ndarray, L: float, closed: bool, cfg: abi.RlCfg
     c.max_outer_iters = 0
     prob = abi.Problem(center=path, L=L, inner_seg=np.zeros((0, 4)), outer_seg=np.zeros((0, 4)), closed=closed)
     return run_oracle(prob, c, B=1, modes=(False, True))[1]
+
+
+def oracle_format_rows(table: np.ndarray) -> bytes:
+    T = np.ascontiguousarray(table, dtype=np.float64)
+    rows, cols = T.shape
+    cap = rows * cols * 64 + 1
+    buf = C.create_string_buffer(cap)
+    n = oracle().oracle_format_rows(T.ctypes.data_as(C.POINTER(C.c_double)), rows, cols, buf, cap)
+    assert n >= 0
+    return buf.raw[:n]

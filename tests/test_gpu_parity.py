@@ -410,7 +410,57 @@ def test_pipeline_csvs_match_reference_cli(tmp_path):
         assert open(base + suffix, "rb").read() == ref, suffix
 
 
-def test_errors_fail_loudly():
+def _fmt_reference(x: float) -> str:
+    """glibc "%.9f" (Python's correctly rounded formatting agrees, except that glibc
+    spells a negative NaN "-nan")."""
+    if np.isnan(x):
+        return "-nan" if np.signbit(x) else "nan"
+    return f"{x:.9f}"
+
+
+def test_format_csv_matches_glibc():
+    """rl_format_csv vs "%.9f" on ties, signed zeros, carries,
+    subnormals, inf/nan and random magnitudes."""
+    _lib_or_skip()
+    rng = np.random.default_rng(0)
+    edge = [0.0, -0.0, 0.0009765625, 0.0029296875, -0.0009765625, 1.0000000005, 0.9999999995, 2.5e-10, 7.5e-10,
+            5e-10, -5e-10, 1e-300, -1e-300, 5e-324, 9.199999e9, -9.199999e9, 123456.0009765625, 999999999.9999999995,
+            float("inf"), float("-inf"), float("nan"), -float("nan"), 1.5, -2.5, 0.1, 1e-9, 1e-10, 4.9999999999e-10]
+    ties = [(2 * k + 1) / 2 ** 11 for k in range(200)] + [k / 1024 for k in range(-300, 300)]
+    rnd = list(rng.normal(size=4000) * 10.0 ** rng.integers(-12, 9, size=4000))
+    rnd += list(rng.integers(-10 ** 15, 10 ** 15, size=2000) / 10 ** 9)       # 9-decimal grid values
+    vals = np.array(edge + ties + rnd, dtype=np.float64)
+    cols = 7
+    pad = (-len(vals)) % cols
+    vals = np.concatenate([vals, np.zeros(pad)])
+    T = vals.reshape(-1, cols)
+    text, offs = raceline.format_table(T, return_offsets=True)
+    want = "".join(",".join(_fmt_reference(v) for v in row) + "\n" for row in T).encode()
+    assert text == want
+    assert offs[-1] == len(want) and offs[0] == 0
+    big = np.array([[9.3e9]])
+    with pytest.raises(raceline.RacelineError) as ei:
+        raceline.format_table(big)
+    assert ei.value.code == abi.RL_ETOOBIG
+
+
+def test_batch_csv_writer_matches_per_instance(tmp_path):
+    """One GPU formatting pass for B instances == the per-instance writer, byte for byte."""
+    _lib_or_skip()
+    case = O.load_case("track_training_map")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    mc, _ = raceline.optimize_batch(prob, cfg, np.arange(6, dtype=np.uint64), 6, mintime=False)
+    bases = [str(tmp_path / f"b{i}") for i in range(6)]
+    raceline.write_batch_raceline_with_geom(bases, mc, float(case["L"]), cfg, s0=float(case["s0"]))
+    for b in range(6):
+        res = raceline.MinCurvResult(raceline=np.stack([mc.x[b], mc.y[b]], 1), heading=mc.heading[b],
+                                     curvature=mc.kappa[b], alpha_total=mc.alpha_total[b], alpha_last=mc.alpha_last[b])
+        ref_base = str(tmp_path / f"r{b}")
+        raceline.write_raceline_csvs(ref_base, res, float(case["L"]), cfg, s0=float(case["s0"]))
+        assert open(bases[b] + "_raceline_with_geom.csv", "rb").read() == open(ref_base + "_raceline_with_geom.csv", "rb").read()
+
+
+
     _lib_or_skip()
     case = O.load_case("track_training_map")
     prob = O.case_problem(case)

@@ -191,3 +191,10 @@ def test_oracle_lap_eval_bit_exact(tag):
         assert mt.lap[0] == float(f["lap"])
         for k in ("heading", "kappa", "v", "ax"):
             np.testing.assert_array_equal(getattr(mt, k)[0], f[k], err_msg=f"{tag}.{name}.{k}")
+
+
+def test_oracle_format_rows_matches_reference_csv():
+    """glibc "%.9f" rows of the step-6 fixture == the reference's own CSV body."""
+    case = O.load_geom_case("training_map")
+    body = case["_csv"].split(b"\n", 1)[1]
+    assert O.oracle_format_rows(case["rows"]) == body
