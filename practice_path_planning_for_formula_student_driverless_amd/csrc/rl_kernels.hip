@@ -195,7 +195,9 @@ struct MinWaves {
                                  : ((T >= 512) ? 1 : (T == 64 ? 4 : 2));
 };
 
-template <int K, int T, bool CLOSED, bool MT>
+// RAGGED: N % K != 0, i.e. one thread holds a partial chunk (decided per launch; the
+// exact-multiple version carries no partial-chunk bookkeeping)
+template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
 __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel(KParams p) {
     constexpr int NW = T / 64;
     __shared__ Smem<K, T> sm;
@@ -208,16 +210,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     const int b = blockIdx.x;
     const int N = p.N;
     const int base = tid * K;
-    const int cnt = min(K, max(0, N - base));
     const int Ta = (N + K - 1) / K;
     const bool active = tid < Ta;
+    const int cnt = min(K, max(0, N - base));           // samples of this thread
     const int cntL = N - (Ta - 1) * K;                  // samples of the last active thread
     // wave-uniform: does this wave hold the (only) partial chunk?  Every other
     // lane is either full (cnt == K) or inactive, and inactive lanes carry exact
     // zeros (coefficients, corridor, state, neighbour values), so their sums
     // need no masking.
     const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-    const bool part_wave = (cntL != K) && (((Ta - 1) >> 6) == wid_u);
+    const bool part_wave = RAGGED && (cntL != K) && (((Ta - 1) >> 6) == wid_u);
     // wave-uniform: this wave holds the last active thread or lies beyond it
     const bool tail_wave = wid_u >= ((Ta - 1) >> 6);
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         const double first = a[0], last = a[K - 1];
         *((lane == 0) ? &sm.eF[slot][wid] : &sm.sink[lane]) = first;
         *((lane == 63) ? &sm.eL[slot][wid] : &sm.sink[lane]) = last;
-        if (cntL == K) {
+        if (!RAGGED || cntL == K) {
             *((tid == Ta - 1) ? &sm.wL[slot] : &sm.sink[lane]) = last;
         } else if (part_wave) {
             const double lv = pick(a, cntL - 1);
@@ -888,7 +890,10 @@ int debug_stamps(unsigned long long* host, int nblocks) {
 // ------------------------------------------------------------------ launcher
 template <int K, int T, bool CL, bool MT>
 static hipError_t launch_t(const KParams& p, hipStream_t st) {
-    hipLaunchKernelGGL((rl_optimize_kernel<K, T, CL, MT>), dim3(p.B), dim3(T), 0, st, p);
+    if (p.N % K)
+        hipLaunchKernelGGL((rl_optimize_kernel<K, T, CL, MT, true>), dim3(p.B), dim3(T), 0, st, p);
+    else
+        hipLaunchKernelGGL((rl_optimize_kernel<K, T, CL, MT, false>), dim3(p.B), dim3(T), 0, st, p);
     return hipGetLastError();
 }
 template <int K, int T>
