@@ -839,14 +839,23 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
+                // std::min(hi, std::max(lo, ai)) (ref:731) as selects: v_min/v_max_f64
+                // would return the other zero when lo = -0 / hi = +0 meet a zero, and
+                // alpha_last is printed with its sign (ref:1372).  In phases, with each
+                // compare in its own lane mask, so no select waits on the compare just
+                // before it (VALU-written mask hazard).
+                double ai[K], mm[K];
+                uint64_t cm[K];
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    double ai = al[k] - step * gr[k];
-                    // std::min(hi, std::max(lo, ai)) (ref:731) as selects: v_min/v_max_f64
-                    // would return the other zero when lo = -0 / hi = +0 meet a zero, and
-                    // alpha_last is printed with its sign (ref:1372)
-                    an[k] = smin(hi[k], smax(lo[k], ai));
-                }
+                for (int k = 0; k < K; ++k) ai[k] = al[k] - step * gr[k];
+#pragma unroll
+                for (int k = 0; k < K; ++k) cm[k] = __builtin_amdgcn_ballot_w64(lo[k] < ai[k]);
+#pragma unroll
+                for (int k = 0; k < K; ++k) mm[k] = __builtin_amdgcn_inverse_ballot_w64(cm[k]) ? ai[k] : lo[k];
+#pragma unroll
+                for (int k = 0; k < K; ++k) cm[k] = __builtin_amdgcn_ballot_w64(mm[k] < hi[k]);
+#pragma unroll
+                for (int k = 0; k < K; ++k) an[k] = __builtin_amdgcn_inverse_ballot_w64(cm[k]) ? mm[k] : hi[k];
                 double Jn = eval_j(an, true, dec);
                 ++evals;
                 if (Jn <= J + armijo_c * dec) {
