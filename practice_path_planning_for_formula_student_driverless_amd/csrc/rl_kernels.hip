@@ -64,11 +64,13 @@ __device__ unsigned long long rl_dbg_stamps[16384][8];
 #endif
 
 // ------------------------------------------------------------ wave primitives
+// x from another lane for patterns where every lane has a source (quad_perm, row_ror):
+// no `old` operand, so no register has to be zeroed first
 template <int CTRL>
 __device__ __forceinline__ double dpp(double x) {
     int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double readlane(double x, int l) {
@@ -78,11 +80,13 @@ __device__ __forceinline__ double readlane(double x, int l) {
 // wave-uniform sum of x over the 64 lanes: DPP butterflies inside each 16-lane row
 // (quad_perm, row_ror:4, row_ror:8), then the four row sums via readlane, combined
 // in a fixed order.  No LDS round trip.
+// row_bcast steps: rows outside ROWS keep an unspecified value.  Only lane 63 of the
+// reduction is read, and those rows never feed it, so no register is zeroed first.
 template <int CTRL, int ROWS>
-__device__ __forceinline__ double dpp_rows(double x) {     // rows outside ROWS read 0
+__device__ __forceinline__ double dpp_rows(double x) {
     int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWS, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROWS, 0xf, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, ROWS, 0xf, false);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, ROWS, 0xf, false);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double wave_sum(double x) {
@@ -90,9 +94,21 @@ __device__ __forceinline__ double wave_sum(double x) {
     x += dpp<0x4E>(x);    // quad_perm [2,3,0,1]
     x += dpp<0x124>(x);   // row_ror:4
     x += dpp<0x128>(x);   // row_ror:8  -> every lane holds its row sum r0..r3
-    x += dpp_rows<0x142, 0xa>(x);   // row_bcast:15 into rows 1,3: r0+r1, r2+r3
+    x += dpp_rows<0x142, 0xa>(x);   // row_bcast:15 into rows 1,3: r0+r1, r2+r3 (rows 0,2: unused)
     x += dpp_rows<0x143, 0xc>(x);   // row_bcast:31 into rows 2,3: lane 63 = (r2+r3)+(r0+r1)
     return readlane(x, 63);
+}
+// two wave sums at once, step by step (each chain fills the other's DPP hazard
+// window); same association as wave_sum, so bit-identical results
+__device__ __forceinline__ void wave_sum2(double& x, double& y) {
+    x += dpp<0xB1>(x);  y += dpp<0xB1>(y);
+    x += dpp<0x4E>(x);  y += dpp<0x4E>(y);
+    x += dpp<0x124>(x); y += dpp<0x124>(y);
+    x += dpp<0x128>(x); y += dpp<0x128>(y);
+    x += dpp_rows<0x142, 0xa>(x); y += dpp_rows<0x142, 0xa>(y);
+    x += dpp_rows<0x143, 0xc>(x); y += dpp_rows<0x143, 0xc>(y);
+    x = readlane(x, 63);
+    y = readlane(y, 63);
 }
 // wave-uniform sum of x on the fp64 matrix core: with B = ones, v_mfma_f64_16x16x4
 // gives each lane the four row sums S_{4g..4g+3} of its 16-lane group g (S_i = Σ_k
@@ -601,7 +617,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #if RL_MFMA_RED
         pJ = wave_sum_mfma(pJ);
 #else
-        pJ = wave_sum(pJ);
+        if (trial) wave_sum2(pJ, pdec);
+        else pJ = wave_sum(pJ);
 #endif
 #ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
         {
@@ -611,8 +628,6 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #endif
 #if RL_MFMA_RED
         if (trial) pdec = wave_sum_mfma(pdec);
-#else
-        if (trial) pdec = wave_sum(pdec);
 #endif
         if (lane == 0) { sm.red[0][wid] = pJ; sm.red[2][wid] = pdec; }
         __syncthreads();
