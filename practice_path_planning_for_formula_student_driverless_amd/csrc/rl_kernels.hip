@@ -249,6 +249,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     const double two_h = 2 * h, hh = h * h;              // ref:602-603 divisors
     const double lam = C.lambda_smooth;
     const double lam2 = 2.0 * lam;                       // ref:673 2.0*lambda_smooth*gsm
+    const double lam_act = active ? lam : 0.0;           // inactive lanes' Σa1² drops out of J
+    const bool is_last = tid == Ta - 1;
     // PGD constants in registers (the cfg lives in global memory the kernel also writes)
     const double step_init = C.step_init, step_min = C.step_min, armijo_c = C.armijo_c;
     const int max_inner = C.max_inner_iters;
@@ -281,10 +283,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         const double ef = sm.eF[slot][(wid + 1 < NW) ? wid + 1 : 0];
         lv = dpp_from_left_or(a[K - 1], el);
         rv = dpp_from_right_or(a[0], ef);
-        if (tail_wave) {
+        // the closed wrap for the last active thread; inactive lanes keep whatever
+        // their neighbours hold (finite) -- their coefficients and bounds are zero,
+        // so only their Σa1² term could leak, and lam_act removes it
+        if (CLOSED && tail_wave) {
             const double e0 = sm.eF[slot][0];
-            if (tid == Ta - 1) rv = e0;
-            if (!active) { lv = 0.0; rv = 0.0; }
+            if (is_last) rv = e0;
         }
     };
     // the last active thread's padding slots take the right neighbour, so every
@@ -600,7 +604,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #pragma unroll
             for (int k = 0; k < K; ++k) acc(k);
         }
-        pJ = __builtin_fma(lam, pJsm, pJ);             // J += λ·Jsm (ref:663 / 883), per lane
+        pJ = __builtin_fma(lam_act, pJsm, pJ);         // J += λ·Jsm (ref:663 / 883), per lane
         xpub(1, q1);
         xpub(2, q2);
         xpub(3, a1v);

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Build A/B pair: librl_base.so from a git revision (default HEAD), librl_new.so
+# from the working tree; both into _lib/variants/ (experiments only).
+set -e
+rev=${1:-HEAD}
+repo=$(cd "$(dirname "$0")/.." && pwd)
+pkg=practice_path_planning_for_formula_student_driverless_amd
+vdir=$repo/$pkg/_lib/variants
+rm -rf "$vdir"; mkdir -p "$vdir"
+tmp=$(mktemp -d)
+git -C "$repo" archive "$rev" $pkg/csrc include | tar -x -C "$tmp"
+python3 - "$repo" "$tmp" "$vdir" <<'PY'
+import sys, os, subprocess
+from concurrent.futures import ThreadPoolExecutor
+repo, tmp, vdir = sys.argv[1:4]
+sys.path.insert(0, repo)
+from practice_path_planning_for_formula_student_driverless_amd import build as B
+pkg = os.path.basename(B.PKG)
+def one(args):
+    root, name = args
+    cwd = os.path.join(root, pkg)
+    inc = os.path.join(root, "include")
+    flags = [f if not f.startswith("-I") or "include" not in f else "-I" + inc for f in B.HIP_FLAGS]
+    out = os.path.join(vdir, f"librl_{name}.so")
+    subprocess.run([B.HIPCC, *flags, "-shared", *B.KERNEL_SRCS, "-o", out], cwd=cwd, check=True)
+    return out
+with ThreadPoolExecutor(2) as ex:
+    for p in ex.map(one, [(tmp, "base"), (repo, "new")]): print("built", p)
+PY
+rm -rf "$tmp"
