@@ -20,6 +20,11 @@ Cases:
                         full-precision rows, plus the reference's own <base>_with_geom.csv text
                         (7 tracks, training_map open, competition_map1 samples=2000);
                         `gen_golden.py --geom` regenerates only these
+  cli_<case>            the whole reference CLI (main.cpp:1598-1714) on cone files: every CSV it
+                        writes, byte for byte (steps 1-5 intermediates, centreline, step 6, both
+                        racelines, the debug dump), as uint8 arrays in one .npz per case; 7 tracks,
+                        training_map open, competition_map1 samples=2000, the 5 shuffled cone sets
+                        and the csv/inner.csv error path. `gen_golden.py --cli` regenerates only these
 Known answers recorded in manifest.json:
   shuffled_identical    *_shuffled.csv inputs give bit-identical hot-path inputs
   error_path            csv/inner.csv+outer.csv -> "not enough midpoints after length filter"
@@ -228,7 +233,74 @@ def debug_fixtures(ref, manifest):
         print("debug", tag, laps)
 
 
+class _Quiet:
+    """fd-level stderr silence around the reference CLI (its main() swaps the stream buffers)."""
+    def __enter__(self):
+        sys.stderr.flush()
+        self.saved = os.dup(2)
+        nul = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(nul, 2)
+        os.close(nul)
+
+    def __exit__(self, *a):
+        os.dup2(self.saved, 2)
+        os.close(self.saved)
+
+
+# (case, inner, outer, --set overrides for fsd_raceline, harness setup)
+def cli_cases():
+    out = []
+    for tr in TRACKS:
+        out.append((tr, f"{tr}_inner.csv", f"{tr}_outer.csv", []))
+    out.append(("training_open", "training_map_inner.csv", "training_map_outer.csv", ["is_closed_track=0"]))
+    out.append(("cmap1_n2000", "competition_map1_inner.csv", "competition_map1_outer.csv",
+                ["use_dynamic_samples=0", "samples=2000"]))
+    for tr in SHUFFLED:
+        out.append((tr + "_shuffled", f"{tr}_inner_shuffled.csv", f"{tr}_outer_shuffled.csv", []))
+    out.append(("error_inner_outer", "inner.csv", "outer.csv", []))
+    return out
+
+
+def cli_fixtures(ref, manifest):
+    """the reference CLI end to end, cfg defaults (debug_dump on) plus the
+    listed overrides; every file it writes next to <base>.csv is kept verbatim."""
+    manifest["cli_cases"] = {}
+    for name, inner, outer, sets in cli_cases():
+        ref.reset()
+        ref.lib.ref_set_debug(1)
+        for kv in sets:
+            k, v = kv.split("=")
+            if k == "is_closed_track":
+                ref.lib.ref_set_closed(int(v))
+            elif k == "samples":
+                ref.lib.ref_set_sampling(0, int(v))
+        d = os.path.join(ref.tmp, "cli_" + name)
+        os.makedirs(d)
+        base = os.path.join(d, "t_centerline")
+        with _Quiet():
+            rc = ref.lib.ref_run_cli(f"{REF_CSV}/{inner}".encode(), f"{REF_CSV}/{outer}".encode(),
+                                     (base + ".csv").encode())
+        err = ref.lib.ref_last_error().decode() if rc != 0 else None
+        files = {}
+        for f in sorted(os.listdir(d)):
+            key = f[len("t_centerline"):].lstrip("_").replace(".csv", "") or "centerline"
+            files[key] = np.frombuffer(open(os.path.join(d, f), "rb").read(), dtype=np.uint8)
+        np.savez_compressed(os.path.join(HERE, f"cli_{name}.npz"), **files)
+        manifest["cli_cases"][name] = {"inner": f"csv/{inner}", "outer": f"csv/{outer}", "set": sets, "rc": rc,
+                                       "error": err, "files": sorted(files), "file": f"cli_{name}.npz"}
+        print("cli", name, rc, err, len(files), "files")
+
+
 def main():
+    if "--cli" in sys.argv:
+        ref = Ref()
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        cli_fixtures(ref, manifest)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        shutil.rmtree(ref.tmp, ignore_errors=True)
+        return
     if "--debug" in sys.argv:
         ref = Ref()
         with open(os.path.join(HERE, "manifest.json")) as f:
@@ -352,6 +424,7 @@ def main():
     manifest["ref_csv"] = {"track": "training_map", "dir": "ref_csv"}
     geom_fixtures(ref, manifest)
     debug_fixtures(ref, manifest)
+    cli_fixtures(ref, manifest)
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

@@ -1,0 +1,154 @@
+"""The C++ host CLI (host/raceline.cpp -> _lib/fsd_raceline) as a drop-in for the
+reference CLI (ref:1598-1714): same usage `inner.csv outer.csv centerline.csv`, same
+files. Fixtures are the reference CLI's own output files (tests/golden/cli_*.npz,
+written by gen_golden.py --cli from the reference compiled where it lies).
+
+* CPU: steps 1-5 (Delaunay, boundary-edge mids, MST ordering, ring reconstruction,
+  spline resample) run on the host. `--stop-after centerline` stops
+  before any GPU call. Every file they write is compared byte for byte: 7 tracks, the
+  open mode, N=2000, the 5 shuffled cone sets, and the error path of csv/inner.csv.
+* GPU: the whole CLI. The step 1-5 files and step 6 (`_with_geom.csv`, rl_geom) must
+  match byte for byte. The raceline, min-time and debug-compare CSVs are compared
+  column-wise at |Δ| <= 1e-4·max|ref| + 1e-9, the north_star tolerance. The CSVs print 9
+  decimals, so the fixture's text is the reference at 5e-10 resolution. Bytes must also
+  be equal where the earlier parity work established it (training_map).
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+CSV = os.path.join(GOLD, "cones")
+EXE = os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd", "_lib", "fsd_raceline")
+MANIFEST = json.load(open(os.path.join(GOLD, "manifest.json")))
+CASES = MANIFEST["cli_cases"]
+
+STEP15 = ["centerline", "all_points", "tri_raw_idx", "edges_all_idx", "edges_labeldiff_idx",
+          "edges_labeldiff_kept_idx", "mids_ordered", "inner_from_mids", "outer_from_mids", "mids_raw"]
+NUMERIC = ["raceline", "raceline_with_geom", "mintime_raceline", "mintime_with_geom", "debug_compare_paths"]
+BYTE_EXACT_ALL = {"training_map"}
+
+
+def _exe():
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    return EXE
+
+
+def _fixture(name):
+    with np.load(os.path.join(GOLD, CASES[name]["file"]), allow_pickle=False) as z:
+        return {k: z[k].tobytes() for k in z.files}
+
+
+def _run(name, tmp_path, extra=()):
+    c = CASES[name]
+    out = tmp_path / "t_centerline.csv"
+    cmd = [_exe(), os.path.join(CSV, os.path.basename(c["inner"])), os.path.join(CSV, os.path.basename(c["outer"])),
+           str(out)]
+    for kv in c["set"]:
+        cmd += ["--set", kv]
+    cmd += ["--set", "verbose=0", *extra]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120)
+    files = {}
+    for f in os.listdir(tmp_path):
+        key = f[len("t_centerline"):].lstrip("_").replace(".csv", "") or "centerline"
+        files[key] = (tmp_path / f).read_bytes()
+    return r, files
+
+
+def _table(b: bytes):
+    lines = [ln for ln in b.decode().splitlines() if ln]
+    header = None
+    try:
+        float(lines[0].split(",")[0])
+    except (IndexError, ValueError):
+        header, lines = (lines[0], lines[1:]) if lines else (None, lines)
+    return header, np.array([[float(v) for v in ln.split(",")] for ln in lines], dtype=np.float64)
+
+
+def _first_diff(a: bytes, b: bytes):
+    la, lb = a.decode().splitlines(), b.decode().splitlines()
+    for i, (x, y) in enumerate(zip(la, lb)):
+        if x != y:
+            return f"line {i}: got {x!r} want {y!r}"
+    return f"line counts {len(la)} vs {len(lb)}"
+
+
+OK_CASES = sorted(k for k, v in CASES.items() if v["rc"] == 0)
+
+
+def test_fixture_inputs_present():
+    for name, c in CASES.items():
+        for k in ("inner", "outer"):
+            assert os.path.exists(os.path.join(CSV, os.path.basename(c[k]))), (name, c[k])
+
+
+@pytest.mark.parametrize("name", OK_CASES)
+def test_steps_1_to_5_byte_identical(name, tmp_path):
+    """Host steps 1-5 write exactly the reference's intermediate CSVs and centreline."""
+    r, files = _run(name, tmp_path, ["--stop-after", "centerline"])
+    assert r.returncode == 0, r.stderr
+    ref = _fixture(name)
+    for key in STEP15:
+        assert key in files, f"{name}: {key} not written"
+        assert files[key] == ref[key], f"{name}/{key}: {_first_diff(files[key], ref[key])}"
+    # nothing past step 5 is written without the GPU
+    assert "with_geom" not in files and "raceline" not in files
+
+
+def test_shuffled_cones_give_the_same_centreline(tmp_path):
+    """Known answer: shuffled cone files give identical hot-path inputs."""
+    for tr in ("competition_map1", "competition_map2", "competition_map3", "competition_map_testday1",
+               "competition_map_testday2"):
+        a, b = _fixture(tr), _fixture(tr + "_shuffled")
+        for key in ("centerline", "inner_from_mids", "outer_from_mids", "with_geom"):
+            assert a[key] == b[key], (tr, key)
+
+
+def test_error_path_matches_reference(tmp_path):
+    """csv/inner.csv + csv/outer.csv: 'not enough midpoints after length filter' (ref:1124-1126),
+    after the same partial files (all points, triangles, edge lists, mids_raw)."""
+    name = "error_inner_outer"
+    r, files = _run(name, tmp_path, ["--stop-after", "centerline"])
+    assert r.returncode != 0
+    assert CASES[name]["error"] in r.stderr
+    ref = _fixture(name)
+    assert sorted(files) == sorted(ref)
+    for key in ref:
+        assert files[key] == ref[key], f"{key}: {_first_diff(files[key], ref[key])}"
+
+
+def test_cli_usage_and_knobs(tmp_path):
+    r = subprocess.run([_exe()], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    assert r.returncode == 1 and "Usage" in r.stderr
+    r = subprocess.run([_exe(), "a", "b", "c", "--set", "no_such_knob=1"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True)
+    assert r.returncode != 0 and "unknown cfg knob" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", OK_CASES)
+def test_full_cli_matches_reference(name, tmp_path):
+    r, files = _run(name, tmp_path)
+    assert r.returncode == 0, r.stderr
+    ref = _fixture(name)
+    assert sorted(files) == sorted(ref), (sorted(files), sorted(ref))
+    for key in STEP15 + ["with_geom"]:
+        assert files[key] == ref[key], f"{name}/{key}: {_first_diff(files[key], ref[key])}"
+    for key in NUMERIC:
+        hg, g = _table(files[key])
+        hr, w = _table(ref[key])
+        assert hg == hr and g.shape == w.shape, (name, key, g.shape, w.shape)
+        nan_g, nan_w = np.isnan(g), np.isnan(w)
+        assert np.array_equal(nan_g, nan_w), (name, key, "NaN pattern")
+        g, w = np.where(nan_w, 0.0, g), np.where(nan_w, 0.0, w)
+        tol = 1e-4 * np.max(np.abs(w), axis=0) + 1e-9
+        err = np.max(np.abs(g - w), axis=0)
+        assert np.all(err <= tol), f"{name}/{key}: columns {np.flatnonzero(err > tol)} err {err} tol {tol}"
+        if name in BYTE_EXACT_ALL:
+            assert files[key] == ref[key], f"{name}/{key}: {_first_diff(files[key], ref[key])}"
+    assert "[mintime] Estimated laptime:" in r.stderr
