@@ -244,6 +244,16 @@ int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double
 int rl_format_csv(const double* table, int64_t rows, int32_t cols, int32_t device, char* out, int64_t out_cap,
                   int64_t* out_len, int64_t* row_offsets);
 
+/* ------------------------------------------------------------ corridor
+ * The optimisers' first corridor (ref:692-711) for the path prob->center_xy:
+ * normals_from_points_generic (ref:581-593), then per sample
+ *   hi = max(0, dpos - guard), lo = -max(0, dneg - guard),
+ *   guard = prob->veh_width*0.5 + cfg->safety_margin_m,
+ * dpos / dneg the safe_ray distances (ref:694-699) along +n / -n to the nearer ring.
+ * The same device code as the optimiser's corridor passes (rl_corridor.h), run in
+ * the optimiser's scan mapping.  lo, hi: [N] host buffers.  Returns RL_OK or RL_E*. */
+int rl_corridor(const rl_problem* prob, const rl_cfg* cfg, int32_t device, double* lo, double* hi);
+
 /* ------------------------------------------------------------- runtime */
 int         rl_device_count(void);
 const char* rl_last_error(void);

@@ -522,6 +522,22 @@ int oracle_optimize(const rl_problem* pr, const rl_cfg* cfg, int32_t n_cfg, cons
     return oracle_optimize_range(pr, cfg, n_cfg, seeds, B, 0, B, out_mc, out_mt);
 }
 
+/* The optimisers' first corridor for the path pr->center_xy (ref:692-711): normals,
+ * then the corridor block with guard = pr->veh_width*0.5 + safety_margin_m.  Checker
+ * of rl_corridor. */
+int oracle_corridor(const rl_problem* pr, const rl_cfg* cfg, double* lo, double* hi) {
+    const int N = pr->N;
+    if (N <= 0) return RL_OK;
+    double* b = (double*)malloc(sizeof(double) * 4 * (size_t)N);
+    if (!b) return RL_ENOMEM;
+    double *Px = b, *Py = b + N, *nx = b + 2 * N, *ny = b + 3 * N;
+    for (int i = 0; i < N; ++i) { Px[i] = pr->center_xy[2 * i]; Py[i] = pr->center_xy[2 * i + 1]; }
+    normals(Px, Py, N, pr->closed != 0, nx, ny);
+    corridor(Px, Py, nx, ny, N, pr, pr->veh_width, cfg->safety_margin_m, lo, hi);
+    free(b);
+    return RL_OK;
+}
+
 /* ---------------------------------------------------------- step 6: geometry */
 /* Spline1D::eval_with_deriv, ref:435-445 */
 static void spline_eval_d(const rl_spline* sp, double si, double* f, double* fp, double* fpp) {

@@ -364,6 +364,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_geom.argtypes = [C.POINTER(RlGeomProblem), C.POINTER(RlCfg), C.c_int32, C.POINTER(C.c_double),
                             C.POINTER(C.c_float)]
     lib.rl_geom.restype = C.c_int
+    if hasattr(lib, "rl_corridor"):      # absent only in older experiment builds (A/B bases)
+        lib.rl_corridor.argtypes = [C.POINTER(RlProblem), C.POINTER(RlCfg), C.c_int32, C.POINTER(C.c_double),
+                                    C.POINTER(C.c_double)]
+        lib.rl_corridor.restype = C.c_int
     lib.rl_lap_eval.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32, C.c_int32, C.c_int32,
                                 C.POINTER(RlCfg), C.c_int32, C.c_int32, C.POINTER(RlOut), C.POINTER(C.c_float)]
     lib.rl_lap_eval.restype = C.c_int

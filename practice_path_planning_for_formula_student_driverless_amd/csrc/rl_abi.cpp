@@ -56,6 +56,7 @@ struct RingHost {
     std::vector<double> vtx;        // [M][2]
     std::vector<rl::SegRec> rec;    // [M]
     std::vector<uint32_t> flag;     // [M/32]
+    std::vector<double> blk;        // [M/8][4] block circles (rl_corridor.h block culling)
     int M = 0, E = 0;
     double dl0 = 0;
 };
@@ -92,6 +93,36 @@ RingHost make_ring(const double* s, int E) {
     // exact expressions propagate the values like the reference
     R.dl0 = 4e-12 * (1.0 + vmax) + 4e-15 * rv;
     if (!(vmax == vmax) || !(rv == rv)) R.dl0 = nan;
+    // Per block of RL_BLK entries: a circle holding both endpoints of every segment that
+    // ends in the block (the start point of the segment ending at v is entry v-1's
+    // vertex, bit for bit). R = -1: no segment ends there; R = +inf: a non-finite
+    // coordinate, so the block is never skipped.
+    const int nb = R.M / rl::RL_BLK;
+    R.blk.assign((size_t)4 * nb, 0.0);
+    for (int b = 0; b < nb; ++b) {
+        double px[2 * rl::RL_BLK], py[2 * rl::RL_BLK];
+        int n = 0;
+        for (int v = b * rl::RL_BLK; v < (b + 1) * rl::RL_BLK; ++v) {
+            if (!ends[v]) continue;
+            px[n] = R.rec[v].x0; py[n++] = R.rec[v].y0;
+            px[n] = R.vtx[2 * v]; py[n++] = R.vtx[2 * v + 1];
+        }
+        double* o = &R.blk[(size_t)4 * b];
+        if (n == 0) { o[2] = -1.0; continue; }
+        bool finite = true;
+        double x0 = px[0], x1 = px[0], y0 = py[0], y1 = py[0];
+        for (int j = 0; j < n; ++j) {
+            finite = finite && std::isfinite(px[j]) && std::isfinite(py[j]);
+            x0 = std::min(x0, px[j]); x1 = std::max(x1, px[j]);
+            y0 = std::min(y0, py[j]); y1 = std::max(y1, py[j]);
+        }
+        const double cx = 0.5 * (x0 + x1), cy = 0.5 * (y0 + y1);
+        double rad = 0.0;
+        for (int j = 0; j < n; ++j) rad = std::max(rad, std::hypot(px[j] - cx, py[j] - cy));
+        o[0] = cx;
+        o[1] = cy;
+        o[2] = finite ? rad * (1.0 + 1e-9) + 1e-12 * (1.0 + std::fabs(cx) + std::fabs(cy)) : INFINITY;
+    }
     return R;
 }
 
@@ -125,6 +156,7 @@ struct rl_plan {
     double* d_vtx = nullptr;
     rl::SegRec* d_rec = nullptr;
     uint32_t* d_flag = nullptr;
+    double* d_blk = nullptr;
     int ring_M[2] = {0, 0};
     double ring_dl0[2] = {0, 0};
     rl_cfg* d_cfg = nullptr;
@@ -303,7 +335,7 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
     if (Ls && (rc = p->alloc(&p->d_Ls, (size_t)B))) return cleanup(rc);
     if ((rc = p->alloc(&p->d_center, centers ? 2 * N * (size_t)B : 2 * N)) || (rc = p->alloc(&p->d_vtx, 2 * Mt)) ||
         (rc = p->alloc(&p->d_rec, Mt)) || (rc = p->alloc(&p->d_flag, Mt / 32)) ||
-        (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
+        (rc = p->alloc(&p->d_blk, 4 * (Mt / rl::RL_BLK))) || (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
         return cleanup(rc);
     hipStream_t st = p->own_stream;
     if (p->N > 0 && hipMemcpyAsync(p->d_center, centers ? centers : prob->center_xy,
@@ -316,7 +348,9 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
         if (R.M == 0) continue;
         if (hipMemcpyAsync(p->d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(p->d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st))
+            hipMemcpyAsync(p->d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_blk + 4 * (size_t)(off / rl::RL_BLK), R.blk.data(), R.blk.size() * sizeof(double),
+                           hipMemcpyHostToDevice, st))
             return cleanup(fail(RL_EHIP, "upload rings"));
         // the copies read the host vectors: wait before they go out of scope
         if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(RL_EHIP, "upload sync"));
@@ -383,6 +417,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
             kp.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
             kp.ring[r].rec = p->d_rec + off;
             kp.ring[r].flag = p->d_flag + off / 32;
+            kp.ring[r].blk = p->d_blk + 4 * (size_t)(off / rl::RL_BLK);
             kp.ring[r].M = p->ring_M[r];
             kp.ring[r].E = r == 0 ? p->Ei : p->Eo;
             kp.ring[r].dl0 = p->ring_dl0[r];
@@ -432,6 +467,71 @@ int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, i
 }
 
 // pipeline::compute_geom_and_save rows (ref:1295-1335) on the device
+int rl_corridor(const rl_problem* prob, const rl_cfg* cfg, int32_t device, double* lo, double* hi) {
+    if (!prob || !cfg || !lo || !hi) return fail(RL_EINVAL, "rl_corridor: NULL argument");
+    if (prob->N < 0 || (prob->N > 0 && !prob->center_xy)) return fail(RL_EINVAL, "rl_corridor: bad centre");
+    if (prob->Ei < 0 || prob->Eo < 0 || (prob->Ei > 0 && !prob->inner_seg) || (prob->Eo > 0 && !prob->outer_seg))
+        return fail(RL_EINVAL, "rl_corridor: bad segments");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    const int N = prob->N;
+    if (N == 0) return RL_OK;
+    RingHost rh[2] = {make_ring(prob->inner_seg, prob->Ei), make_ring(prob->outer_seg, prob->Eo)};
+    const size_t Mt = (size_t)rh[0].M + rh[1].M;
+    std::vector<void*> mem;
+    auto dalloc = [&](size_t bytes) -> void* {
+        void* q = nullptr;
+        if (hipMalloc(&q, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+        mem.push_back(q);
+        return q;
+    };
+    auto release = [&](int code) {
+        for (void* q : mem) hipFree(q);
+        return code;
+    };
+    double* d_c = (double*)dalloc(2 * (size_t)N * sizeof(double));
+    double* d_out = (double*)dalloc(2 * (size_t)N * sizeof(double));
+    double* d_vtx = (double*)dalloc(2 * Mt * sizeof(double));
+    rl::SegRec* d_rec = (rl::SegRec*)dalloc(Mt * sizeof(rl::SegRec));
+    uint32_t* d_flag = (uint32_t*)dalloc(Mt / 32 * sizeof(uint32_t));
+    double* d_blk = (double*)dalloc(4 * (Mt / rl::RL_BLK) * sizeof(double));
+    if (!d_c || !d_out || !d_vtx || !d_rec || !d_flag || !d_blk) return release(fail(RL_ENOMEM, "rl_corridor: hipMalloc failed"));
+    rl::CorrParams c{};
+    c.center = d_c;
+    c.N = N;
+    c.closed = prob->closed ? 1 : 0;
+    c.guard = prob->veh_width * 0.5 + cfg->safety_margin_m;     // ref:706
+    c.lo = d_out;
+    c.hi = d_out + N;
+    bool ok = hipMemcpy(d_c, prob->center_xy, 2 * (size_t)N * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+    for (int r = 0, off = 0; r < 2; off += rh[r].M, ++r) {
+        const RingHost& R = rh[r];
+        if (R.M)
+            ok = ok &&
+                 hipMemcpy(d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+                 hipMemcpy(d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice) == hipSuccess &&
+                 hipMemcpy(d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess &&
+                 hipMemcpy(d_blk + 4 * (size_t)(off / rl::RL_BLK), R.blk.data(), R.blk.size() * sizeof(double),
+                           hipMemcpyHostToDevice) == hipSuccess;
+        c.ring[r].vtx = (const double2*)(d_vtx + 2 * (size_t)off);
+        c.ring[r].rec = d_rec + off;
+        c.ring[r].flag = d_flag + off / 32;
+        c.ring[r].blk = d_blk + 4 * (size_t)(off / rl::RL_BLK);
+        c.ring[r].M = R.M;
+        c.ring[r].E = R.E;
+        c.ring[r].dl0 = R.dl0;
+    }
+    if (!ok) return release(fail(RL_EHIP, "rl_corridor: upload"));
+    if (rl::launch_corridor(c, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return release(fail(RL_EHIP, "rl_corridor: kernel"));
+    if (hipMemcpy(lo, d_out, (size_t)N * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hi, d_out + N, (size_t)N * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+        return release(fail(RL_EHIP, "rl_corridor: download"));
+    return release(RL_OK);
+}
+
 int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double* rows, float* kernel_ms) {
     if (!gp || !cfg || !rows) return fail(RL_EINVAL, "rl_geom: NULL argument");
     if (gp->Kmax < 0 || gp->denomN == 0) return fail(RL_EINVAL, "rl_geom: Kmax < 0 or denomN == 0");
@@ -476,8 +576,9 @@ int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double
     double* d_vtx = (double*)dalloc(2 * Mt * sizeof(double));
     rl::SegRec* d_rec = (rl::SegRec*)dalloc(Mt * sizeof(rl::SegRec));
     uint32_t* d_flag = (uint32_t*)dalloc(Mt / 32 * sizeof(uint32_t));
+    double* d_blk = (double*)dalloc(4 * (Mt / rl::RL_BLK) * sizeof(double));
     double* d_rows = (double*)dalloc((size_t)nrows * RL_GEOM_COLS * sizeof(double));
-    if (!d_kn || !d_vtx || !d_rec || !d_flag || !d_rows) return release(fail(RL_ENOMEM, "rl_geom: hipMalloc failed"));
+    if (!d_kn || !d_vtx || !d_rec || !d_flag || !d_blk || !d_rows) return release(fail(RL_ENOMEM, "rl_geom: hipMalloc failed"));
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return release(fail(RL_EHIP, "rl_geom: stream"));
@@ -497,12 +598,15 @@ int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double
         if (R.M) {
             if (hipMemcpyAsync(d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice, st) ||
                 hipMemcpyAsync(d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st) ||
-                hipMemcpyAsync(d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st))
+                hipMemcpyAsync(d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st) ||
+                hipMemcpyAsync(d_blk + 4 * (size_t)(off / rl::RL_BLK), R.blk.data(), R.blk.size() * sizeof(double),
+                               hipMemcpyHostToDevice, st))
                 return finish(fail(RL_EHIP, "rl_geom: upload rings"));
         }
         g.ring[r].vtx = (const double2*)(d_vtx + 2 * (size_t)off);
         g.ring[r].rec = d_rec + off;
         g.ring[r].flag = d_flag + off / 32;
+        g.ring[r].blk = d_blk + 4 * (size_t)(off / rl::RL_BLK);
         g.ring[r].M = R.M;
         g.ring[r].E = R.E;
         g.ring[r].dl0 = R.dl0;
@@ -683,6 +787,12 @@ int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const 
 #ifdef RL_STAMPS
 // diagnostic builds only: per-phase cycle totals of the last launch (see rl_kernels.hip)
 int rl_debug_stamps(unsigned long long* host, int nblocks) { return rl::debug_stamps(host, nblocks); }
+int rl_debug_stamps_stream(unsigned long long* host, int nblocks) { return rl::debug_stamps_stream(host, nblocks); }
+#endif
+#ifdef RL_COUNT
+// diagnostic builds only: corridor work counters of the stream kernel's translation unit
+int rl_debug_counts(unsigned long long* host, int reset) { return rl::debug_counts(host, reset); }
+int rl_debug_counts_geom(unsigned long long* host, int reset) { return rl::debug_counts_geom(host, reset); }
 #endif
 
 }  // extern "C"

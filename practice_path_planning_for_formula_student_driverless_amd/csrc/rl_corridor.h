@@ -45,9 +45,31 @@ struct RingDesc {
     const double2* vtx;       // [M] entry vertex (NaN for padding)
     const SegRec* rec;        // [M] record of the segment ending at the entry
     const uint32_t* flag;     // [M/32] bit (31-j): entry 32b+j ends a segment
+    const double* blk;        // [M/8][4] block circles (cx, cy, R, 0); R < 0: no segment ends in the block
     int32_t M, E;             // padded entry count, segment count
     double dl0;               // 4e-12*(1+Vmax) + 4e-15*Rv
 };
+
+// Block culling. Entries come in blocks of 8. The host gives each block a circle (C, R)
+// that contains both endpoints of every segment ending in the block (rl_abi.cpp
+// make_ring), so every point of those segments lies within R of C.
+//  * Ray filter: |n x (V - C)| <= |n| R for every such vertex V. If the centre's side
+//    value satisfies |c_C| > R(1+1e-9) + 2 dl, every endpoint's computed side value is
+//    beyond dl on the same side (the error of a computed side value is below dl/6), so
+//    no segment of the block is a candidate for that sample.
+//  * Fallback: the distance to any segment of the block is >= |q - C| - R.
+// A block is skipped only when every lane's samples skip it, so the entry loop stays
+// wave-uniform. What survives is exactly what the entry tests would keep.
+constexpr int RL_BLK = 8;
+
+// Diagnostic build only (-DRL_COUNT=1): corridor work counters (lane-level events),
+// summed with atomics into a device array no other code reads.
+#ifdef RL_COUNT
+static __device__ unsigned long long rl_dbg_count[8];   // one per translation unit
+#define RL_CNT(slot, n) atomicAdd(&rl_dbg_count[slot], (unsigned long long)(n))
+#else
+#define RL_CNT(slot, n) do {} while (0)
+#endif
 
 // exact rayIntersectSegment for +n and -n at once, folded into the running minima
 __device__ __forceinline__ void ray_exact(double x0, double y0, double vx, double vy, double qx, double qy,
@@ -96,6 +118,7 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
                                           double (&bp)[CK], double (&bn)[CK], double (&ub2)[CK]) {
     cdbl* V = as_cdbl(R.vtx);              // [M][2]
     cu32* F = as_cu32(R.flag);
+    cdbl* BK = as_cdbl(R.blk);             // [M/8][4]
     const SegRec* __restrict__ S = R.rec;  // per-lane (divergent) reads
     double dl[CK], g[CK];
     uint64_t pp[CK], pn[CK];       // side masks of the previous entry (wave lane masks, SGPR)
@@ -107,23 +130,62 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
         bp[k] = bn[k] = ub2[k] = INFINITY;
         pp[k] = pn[k] = 0ull;
     }
+    bool prev_ok = false;          // pp/pn hold the sides of the entry just before the next one
     for (int b0 = 0; b0 < R.M; b0 += 32) {
         uint32_t w[CK];
 #pragma unroll
         for (int k = 0; k < CK; ++k) w[k] = 0u;
-#pragma unroll 8
-        for (int j = 0; j < 32; ++j) {
-            const double vx = V[2 * (b0 + j)], vy = V[2 * (b0 + j) + 1];
+        // which of the word's 4 blocks some lane's ray line may cross (wave-uniform)
+        uint32_t visit = 0u;
 #pragma unroll
-            for (int k = 0; k < CK; ++k) {
-                const double c = __builtin_fma(ux[k], vy, -__builtin_fma(uy[k], vx, g[k]));
-                const uint64_t P = __builtin_amdgcn_ballot_w64(c > dl[k]);
-                const uint64_t Q = __builtin_amdgcn_ballot_w64(c < -dl[k]);
-                const uint64_t cand = ~((P & pp[k]) | (Q & pn[k]));
-                w[k] = (w[k] << 1) | (uint32_t)__builtin_amdgcn_inverse_ballot_w64(cand);
-                pp[k] = P;
-                pn[k] = Q;
+        for (int q = 0; q < 32 / RL_BLK; ++q) {
+            cdbl* bk = BK + 4 * ((b0 / RL_BLK) + q);
+            const double cx = bk[0], cy = bk[1], rb = bk[2];
+            bool need = false;
+            if (rb >= 0.0) {
+#pragma unroll
+                for (int k = 0; k < CK; ++k) {
+                    const double c = __builtin_fma(ux[k], cy, -__builtin_fma(uy[k], cx, g[k]));
+                    need |= act[k] && !(fabs(c) > rb * (1.0 + 1e-9) + 2.0 * dl[k]);
+                }
             }
+            if (__any(need)) visit |= 1u << q;
+        }
+        if (threadIdx.x % 64 == 0) { RL_CNT(0, 4); RL_CNT(1, __popc(visit)); }
+        if (visit == 0u) { prev_ok = false; continue; }
+#pragma unroll
+        for (int q = 0; q < 32 / RL_BLK; ++q) {
+            if (!((visit >> q) & 1u)) {
+#pragma unroll
+                for (int k = 0; k < CK; ++k) w[k] <<= RL_BLK;
+                prev_ok = false;
+                continue;
+            }
+            const int e0 = b0 + q * RL_BLK;
+            if (!prev_ok && e0 > 0) {      // sides of the entry before the block
+                const double vx = V[2 * (e0 - 1)], vy = V[2 * (e0 - 1) + 1];
+#pragma unroll
+                for (int k = 0; k < CK; ++k) {
+                    const double c = __builtin_fma(ux[k], vy, -__builtin_fma(uy[k], vx, g[k]));
+                    pp[k] = __builtin_amdgcn_ballot_w64(c > dl[k]);
+                    pn[k] = __builtin_amdgcn_ballot_w64(c < -dl[k]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < RL_BLK; ++j) {
+                const double vx = V[2 * (e0 + j)], vy = V[2 * (e0 + j) + 1];
+#pragma unroll
+                for (int k = 0; k < CK; ++k) {
+                    const double c = __builtin_fma(ux[k], vy, -__builtin_fma(uy[k], vx, g[k]));
+                    const uint64_t P = __builtin_amdgcn_ballot_w64(c > dl[k]);
+                    const uint64_t Q = __builtin_amdgcn_ballot_w64(c < -dl[k]);
+                    const uint64_t cand = ~((P & pp[k]) | (Q & pn[k]));
+                    w[k] = (w[k] << 1) | (uint32_t)__builtin_amdgcn_inverse_ballot_w64(cand);
+                    pp[k] = P;
+                    pn[k] = Q;
+                }
+            }
+            prev_ok = true;
         }
         const uint32_t f = F[b0 >> 5];
 #pragma unroll
@@ -137,9 +199,11 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
                 const SegRec* s = S + b0 + j[k];
                 x0[k] = s->x0; y0[k] = s->y0; sx[k] = s->vx; sy[k] = s->vy;
             }
+            if (threadIdx.x % 64 == 0) RL_CNT(2, 1);          // walk iterations (wave)
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
                 if (h[k]) {
+                    RL_CNT(3, 1);                                 // exact ray tests (lane)
                     ray_exact(x0[k], y0[k], sx[k], sy[k], qx[k], qy[k], ux[k], uy[k], bp[k], bn[k]);
                     // any segment endpoint bounds the point-to-segment minimum from above
                     const double ax = qx[k] - x0[k], ay = qy[k] - y0[k];
@@ -153,13 +217,15 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
 
 // minDistanceToSegments_global (ref:501-512) for the samples with need[k], exact for
 // every sample whose minimum is <= rad[k] (md[k] = +inf or a value > rad[k] otherwise).
-// One lane-level filter per entry: the samples' bounding circle (centre q0, radius
-// max_k rad[k] + |q_k - q0|_1) against |mid - q0| <= R + half_len.
+// Lane-level filters per block and per entry: the samples' bounding circle (centre q0,
+// radius max_k rad[k] + |q_k - q0|_1) against the block circle, then against
+// |mid - q0| <= R + half_len.
 template <int CK>
 __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
                                              const bool (&need)[CK], const double (&rad)[CK], double (&md)[CK]) {
     cdbl* SR = as_cdbl(R.rec);             // [M][8] SegRec fields (uniform reads)
     cu32* F = as_cu32(R.flag);
+    cdbl* BK = as_cdbl(R.blk);
     const SegRec* __restrict__ S = R.rec;
     const double cx = qx[0], cy = qy[0];
     double Rl = -1.0;
@@ -171,14 +237,29 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
         lneed |= need[k];
     }
     for (int b0 = 0; b0 < R.M; b0 += 32) {
+        uint32_t visit = 0u;
+#pragma unroll
+        for (int q = 0; q < 32 / RL_BLK; ++q) {
+            cdbl* bk = BK + 4 * ((b0 / RL_BLK) + q);
+            const double dx = cx - bk[0], dy = cy - bk[1], rb = bk[2];
+            const double r = (Rl + rb) * (1.0 + 1e-12);
+            const bool nb = lneed && rb >= 0.0 && !(dx * dx + dy * dy > r * r);
+            if (__any(nb)) visit |= 1u << q;
+        }
+        if (threadIdx.x % 64 == 0) { RL_CNT(4, 4); RL_CNT(5, __popc(visit)); }
+        if (visit == 0u) continue;
         uint32_t w = 0u;
-#pragma unroll 8
-        for (int j = 0; j < 32; ++j) {
-            cdbl* sr = SR + 8 * (b0 + j);
-            const double mx = sr[5], my = sr[6], hr = sr[7];
-            const double dx = cx - mx, dy = cy - my, r = Rl + hr;
-            const bool skip = dx * dx + dy * dy > r * r;
-            w = (w << 1) | (uint32_t)!skip;
+#pragma unroll
+        for (int q = 0; q < 32 / RL_BLK; ++q) {
+            if (!((visit >> q) & 1u)) { w <<= RL_BLK; continue; }
+#pragma unroll
+            for (int j = 0; j < RL_BLK; ++j) {
+                cdbl* sr = SR + 8 * (b0 + q * RL_BLK + j);
+                const double mx = sr[5], my = sr[6], hr = sr[7];
+                const double dx = cx - mx, dy = cy - my, r = Rl + hr;
+                const bool skip = dx * dx + dy * dy > r * r;
+                w = (w << 1) | (uint32_t)!skip;
+            }
         }
         w = lneed ? (w & F[b0 >> 5]) : 0u;
         while (__any(w != 0u)) {
@@ -187,6 +268,8 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
             w &= ~(0x80000000u >> j);
             const SegRec* s = S + b0 + j;
             const double x0 = s->x0, y0 = s->y0, sx = s->vx, sy = s->vy, dn = s->denom;
+            if (threadIdx.x % 64 == 0) RL_CNT(6, 1);              // fallback walk iterations (wave)
+            if (h) RL_CNT(7, 1);                                  // exact distance evaluations (lane)
 #pragma unroll
             for (int k = 0; k < CK; ++k)
                 if (h && need[k]) md[k] = smin(md[k], seg_dist_exact(x0, y0, sx, sy, dn, qx[k], qy[k]));

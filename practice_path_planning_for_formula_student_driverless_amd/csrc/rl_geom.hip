@@ -104,4 +104,56 @@ hipError_t launch_geom(const GeomParams& g, hipStream_t st) {
     return hipGetLastError();
 }
 
+// rl_corridor: each lane takes 2 adjacent samples (the optimiser's corridor scan
+// mapping, rl_kernels.hip), normals_from_points_generic at each (ref:581-593) and the
+// exact corridor bounds of rl_corridor.h.
+__global__ __launch_bounds__(256) void rl_corridor_kernel(CorrParams c) {
+    constexpr int CK = 2;
+    const int N = c.N;
+    const int i0 = (blockIdx.x * blockDim.x + threadIdx.x) * CK;
+    double qx[CK], qy[CK], ux[CK], uy[CK], lo[CK], hi[CK];
+    bool act[CK];
+    auto P = [&](int j, int a) { return c.center[2 * j + a]; };
+#pragma unroll
+    for (int k = 0; k < CK; ++k) {
+        const int i = min(i0 + k, N - 1);
+        act[k] = i0 + k < N;
+        double tx, ty;
+        if (N == 1) { tx = 1; ty = 0; }
+        else if (c.closed) {
+            const int ip = (i + 1 == N) ? 0 : i + 1, im = (i == 0) ? N - 1 : i - 1;
+            tx = (P(ip, 0) - P(im, 0)) * 0.5; ty = (P(ip, 1) - P(im, 1)) * 0.5;
+        } else if (i == 0) { tx = P(1, 0) - P(0, 0); ty = P(1, 1) - P(0, 1); }
+        else if (i == N - 1) { tx = P(N - 1, 0) - P(N - 2, 0); ty = P(N - 1, 1) - P(N - 2, 1); }
+        else { tx = (P(i + 1, 0) - P(i - 1, 0)) * 0.5; ty = (P(i + 1, 1) - P(i - 1, 1)) * 0.5; }
+        if (sqrt(tx * tx + ty * ty) < 1e-15) { tx = 1; ty = 0; }
+        const double vx = -ty, vy = tx, n = sqrt(vx * vx + vy * vy);   // geom::normalize ref:132
+        ux[k] = 0.0; uy[k] = 0.0;
+        if (!(n < 1e-15)) { ux[k] = vx / n; uy[k] = vy / n; }
+        qx[k] = P(i, 0);
+        qy[k] = P(i, 1);
+    }
+    corridor_bounds<CK>(c.ring[0], c.ring[1], qx, qy, ux, uy, act, c.guard, lo, hi);
+#pragma unroll
+    for (int k = 0; k < CK; ++k)
+        if (act[k]) { c.lo[i0 + k] = lo[k]; c.hi[i0 + k] = hi[k]; }
+}
+
+#ifdef RL_COUNT
+int debug_counts_geom(unsigned long long* host, int reset) {
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(rl_dbg_count), z, sizeof(z)) == hipSuccess ? 0 : -3;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_count), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -3;
+}
+#endif
+
+hipError_t launch_corridor(const CorrParams& c, hipStream_t st) {
+    if (c.N <= 0) return hipSuccess;
+    const int T = 256, per = T * 2;
+    hipLaunchKernelGGL(rl_corridor_kernel, dim3((c.N + per - 1) / per), dim3(T), 0, st, c);
+    return hipGetLastError();
+}
+
 }  // namespace rl

@@ -53,12 +53,26 @@ struct GeomParams {
     double* rows;
 };
 hipError_t launch_geom(const GeomParams& g, hipStream_t st);
+// rl_corridor (rl_geom.hip): normals of `center` then the corridor bounds of every sample
+struct CorrParams {
+    const double* center;      // [N][2]
+    int32_t N, closed;
+    RingDesc ring[2];
+    double guard;
+    double *lo, *hi;
+};
+hipError_t launch_corridor(const CorrParams& c, hipStream_t st);
 // "%.9f" CSV rows of a [rows][cols] device table (rl_format.hip): 0, -1 (|x| >= 9.2e9),
 // -2 (cap short; *total = needed), -3 (HIP failure)
 int format_rows(const double* table, int64_t rows, int cols, char* out, uint64_t cap, uint64_t* offs,
                 uint64_t* total, hipStream_t st);
 #ifdef RL_STAMPS
 int debug_stamps(unsigned long long* host, int nblocks);
+int debug_stamps_stream(unsigned long long* host, int nblocks);
+#endif
+#ifdef RL_COUNT
+int debug_counts(unsigned long long* host, int reset);
+int debug_counts_geom(unsigned long long* host, int reset);
 #endif
 
 }  // namespace rl

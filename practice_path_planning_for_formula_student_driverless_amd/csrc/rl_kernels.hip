@@ -365,27 +365,40 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             if (k < cnt) { NX[i] = ox; NY[i] = oy; }
         }
     };
-    // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin), CK samples
-    // at a time through the per-lane candidate scan of rl_corridor.h
+    // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin). The scan runs
+    // in its own mapping: pass c gives lane t the CKK adjacent samples from (c*T+t)*CKK,
+    // so a wave holds 64*CKK consecutive samples whose rays are spatially coherent and
+    // the block culling of rl_corridor.h skips most of both rings. The bounds reach their
+    // owner threads through LDS, in the coefficient area, which is free until lin-geom
+    // fills it: slot k*T+t holds (lo, hi) of sample t*K+k.
     auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
         constexpr int CKK = CK < K ? CK : K;
-#pragma unroll
-        for (int c = 0; c < K; c += CKK) {
+        double2* bnd = &sm.u.coef[0][0][0];
+        for (int c0 = 0; c0 < N; c0 += T * CKK) {
+            const int i0 = c0 + tid * CKK;
             double qx[CKK], qy[CKK], ux[CKK], uy[CKK], lc[CKK], hc[CKK];
             bool act[CKK];
 #pragma unroll
             for (int k = 0; k < CKK; ++k) {
-                const int i = own(c + k);
+                const int i = min(i0 + k, N - 1);
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
-                act[k] = c + k < cnt;
+                act[k] = i0 + k < N;
             }
             corridor_bounds<CKK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lc, hc);
 #pragma unroll
             for (int k = 0; k < CKK; ++k) {
-                hi[c + k] = act[k] ? hc[k] : 0.0;
-                lo[c + k] = act[k] ? lc[k] : 0.0;
+                const int i = i0 + k;
+                if (act[k]) bnd[(i % K) * T + i / K] = make_double2(lc[k], hc[k]);
             }
         }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double2 v = bnd[k * T + tid];
+            lo[k] = (k < cnt) ? v.x : 0.0;
+            hi[k] = (k < cnt) ? v.y : 0.0;
+        }
+        __syncthreads();      // the area is written again (v-pass relaxation, coefficients)
     };
 
     // ---- v(s) profile: velocity_profile_forward_backward ref:782-862 ---------

@@ -78,9 +78,28 @@ __device__ __forceinline__ void block_sum_s(SSmem& sm, double (&v)[NV], int lane
 }
 }  // namespace
 
+#ifdef RL_STAMPS
+// Diagnostic build only: per-phase s_memtime totals of each workgroup's wave 0
+__device__ unsigned long long rl_dbg_stamps_s[16384][8];
+#define RL_SSTAMP(slot)                                             \
+    do {                                                            \
+        __builtin_amdgcn_sched_barrier(0);                          \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();       \
+        st_acc[slot] += t_ - st_last;                               \
+        st_last = t_;                                               \
+        __builtin_amdgcn_sched_barrier(0);                          \
+    } while (0)
+#else
+#define RL_SSTAMP(slot) do {} while (0)
+#endif
+
 template <bool CLOSED, bool MT>
 __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs sb) {
     __shared__ SSmem sm;
+#ifdef RL_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int b = blockIdx.x;
     const int N = p.N;
@@ -296,6 +315,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
     const int MO = C.max_outer_iters;
     double* al_p = AL;
     double* an_p = AN;
+    RL_SSTAMP(0);
     for (int outer = 0;; ++outer) {
         __syncthreads();
         if (outer > 0) {                                           // ref:743-746
@@ -310,16 +330,25 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             }
             __syncthreads();
         }
+        RL_SSTAMP(5);
         if (outer < MO) {
             for (int i = tid; i < N; i += TS) normal_at(i);
             __syncthreads();
+            RL_SSTAMP(6);
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
             for (int i = tid; i < N; i += TS) {
+#ifdef RL_EXP_CORR2
+                corridor_at(i, guard);
+#endif
                 corridor_at(i, guard);
                 if (outer == 0 && seed != 0)
                     al_p[i] = smin(HI[i], smax(LO[i], seed_value(seed, i, RL_SEED_SIGMA)));
             }
         }
+#ifdef RL_STAMPS
+        __syncthreads();
+#endif
+        RL_SSTAMP(1);
         if (MT || outer == MO) {
             for (int i = tid; i < N; i += TS) {                    // ref:595-620
                 double xp, yp, xpp, ypp;
@@ -370,6 +399,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
                 }
             }
         }
+        RL_SSTAMP(2);
         if (outer == MO) break;
 
         for (int i = tid; i < N; i += TS) {                        // ref:622-651
@@ -382,6 +412,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             CW[i] = 1.0 / pow15(smax(1e-12, xp * xp + yp * yp));
         }
         __syncthreads();
+        RL_SSTAMP(3);
 
         // one evaluation of the vector `a` (already written and synchronised):
         // J and the Armijo decrease; q1,q2,D1α to global for the gradient
@@ -428,6 +459,9 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             while (bt < 20) {
                 for (int i = tid; i < N; i += TS) an_p[i] = smin(HI[i], smax(LO[i], al_p[i] - step * GR[i]));   // std:: semantics (ref:731)
                 __syncthreads();
+#ifdef RL_EXP_EVAL2
+                (void)eval_j(an_p, true, dec);
+#endif
                 const double Jn = eval_j(an_p, true, dec);
                 ++evals;
                 if (Jn <= J + C.armijo_c * dec) {
@@ -450,8 +484,30 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             if (p.evals) p.evals[(size_t)b * MO + outer] = evals;
             if (p.accepts) p.accepts[(size_t)b * MO + outer] = accepts;
         }
+        RL_SSTAMP(4);
     }
+#ifdef RL_STAMPS
+    if (tid == 0 && b < 16384) {
+        for (int i = 0; i < 8; ++i) rl_dbg_stamps_s[b][i] = st_acc[i];
+    }
+#endif
 }
+
+#ifdef RL_COUNT
+int debug_counts(unsigned long long* host, int reset) {
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(rl_dbg_count), z, sizeof(z)) == hipSuccess ? 0 : -3;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_count), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -3;
+}
+#endif
+#ifdef RL_STAMPS
+int debug_stamps_stream(unsigned long long* host, int nblocks) {
+    if (nblocks > 16384) nblocks = 16384;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_stamps_s), sizeof(unsigned long long) * 8 * nblocks) == hipSuccess ? 0 : -3;
+}
+#endif
 
 template <bool CL, bool MT>
 static hipError_t launch_s(const KParams& p, const StreamBufs& sb, hipStream_t st) {

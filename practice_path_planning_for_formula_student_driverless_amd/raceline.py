@@ -496,6 +496,17 @@ def format_geom_csv(rows: np.ndarray) -> str:
     return "".join(out)
 
 
+def corridor(prob: Problem, cfg: Optional[RlCfg] = None, device: int = 0):
+    """The optimisers' first corridor (ref:692-711) of the path prob.center on the GPU
+    (rl_corridor): normals, then lo/hi per sample with guard = veh_width/2 + margin."""
+    cfg = cfg if cfg is not None else default_cfg()
+    N = prob.N
+    lo, hi = np.zeros(max(N, 1)), np.zeros(max(N, 1))
+    p = prob.as_c()
+    _check(_lib().rl_corridor(C.byref(p), C.byref(cfg), int(device), abi.dptr(lo), abi.dptr(hi)))
+    return lo[:N], hi[:N]
+
+
 def compute_geom(gp: GeomProblem, cfg: Optional[RlCfg] = None, device: int = 0, return_ms: bool = False):
     """Rows of pipeline::compute_geom_and_save (ref:1295-1335) on the GPU (rl_geom):
     [Kmax + emit_closed_duplicate, 9] = s_rel, x, y, heading, curvature, d_in, d_out,

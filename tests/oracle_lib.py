@@ -47,6 +47,9 @@ def oracle() -> C.CDLL:
         lib.oracle_ring_segments.restype = C.c_int
         lib.oracle_geom.argtypes = [C.POINTER(abi.RlGeomProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double)]
         lib.oracle_geom.restype = C.c_int
+        lib.oracle_corridor.argtypes = [C.POINTER(abi.RlProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_double)]
+        lib.oracle_corridor.restype = C.c_int
         lib.oracle_format_rows.argtypes = [C.POINTER(C.c_double), C.c_longlong, C.c_int, C.c_char_p, C.c_longlong]
         lib.oracle_format_rows.restype = C.c_longlong
         _ORACLE = lib
@@ -145,6 +148,15 @@ def run_oracle_geom(gp: abi.GeomProblem, cfg: abi.RlCfg) -> np.ndarray:
     n = oracle().oracle_geom(C.byref(g), C.byref(cfg), rows.ctypes.data_as(C.POINTER(C.c_double)))
     assert n == gp.rows, n
     return rows[: gp.rows]
+
+
+def run_oracle_corridor(prob: abi.Problem, cfg: abi.RlCfg):
+    """oracle_corridor: normals + the first corridor block (ref:692-711) on the CPU."""
+    lo, hi = np.zeros(max(prob.N, 1)), np.zeros(max(prob.N, 1))
+    p = prob.as_c()
+    rc = oracle().oracle_corridor(C.byref(p), C.byref(cfg), abi.dptr(lo), abi.dptr(hi))
+    assert rc == 0, rc
+    return lo[: prob.N], hi[: prob.N]
 
 
 # ------------------------------------------------- debug dump / lap evaluation

@@ -471,3 +471,64 @@ def test_batch_csv_writer_matches_per_instance(tmp_path):
     with pytest.raises(raceline.RacelineError) as ei:
         raceline.optimize_batch(big, cfg, None, 1)
     assert ei.value.code == abi.RL_ETOOBIG
+
+
+def _corridor_cases():
+    """Paths for the corridor check: the bundled tracks (and the same centrelines pushed
+    off by up to ±0.4 m), open mode, N=2000, arbitrary segment lists, tracks hugging
+    a ring, narrow tracks, rings of 1037 segments and the N=10000 oval."""
+    rng = np.random.default_rng(5)
+    out = []
+    for name in ("track_training_map", "track_competition_map1", "track_competition_map2",
+                 "track_competition_map3", "track_competition_map_testday1", "track_competition_map_testday2",
+                 "track_competition_map_testday3", "training_open", "cmap1_n2000", "oval_n10000"):
+        prob = O.case_problem(O.load_case(name))
+        out.append((name, prob))
+        if name.startswith("track_"):
+            c = prob.center + rng.uniform(-0.4, 0.4, prob.center.shape)
+            out.append((name + "+noise", abi.Problem(center=c, L=prob.L, inner_seg=prob.inner_seg,
+                                                     outer_seg=prob.outer_seg, veh_width=prob.veh_width,
+                                                     closed=prob.closed)))
+    base = O.case_problem(O.load_case("track_competition_map2"))
+    for which in ("inner", "outer"):
+        for vname, seg in _segment_variants(getattr(base, f"{which}_seg"), rng).items():
+            kw = dict(center=base.center, L=base.L, inner_seg=base.inner_seg, outer_seg=base.outer_seg,
+                      veh_width=base.veh_width, closed=True)
+            kw[f"{which}_seg"] = seg
+            out.append((f"{which}.{vname}", abi.Problem(**kw)))
+    for radius, width in ((18.25, 4.0), (21.75, 4.0), (20.0, 1.4), (19.0, 2.2)):
+        N = 700
+        t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+        wob = 1 + 0.04 * np.sin(5 * t)
+        center = np.stack([1.4 * radius * wob * np.cos(t), radius * wob * np.sin(t)], axis=1)
+        k = np.linspace(0, 2 * np.pi, 97, endpoint=False)
+        wk = 1 + 0.04 * np.sin(5 * k)
+        ri, ro = 20.0 - width / 2, 20.0 + width / 2
+        inner = np.stack([1.4 * ri * wk * np.cos(k), ri * wk * np.sin(k)], axis=1)
+        outer = np.stack([1.4 * ro * wk * np.cos(k), ro * wk * np.sin(k)], axis=1)
+        for closed in (True, False):
+            out.append((f"off{radius}/{width}/{closed}",
+                        abi.Problem(center=center, L=1.0, inner_seg=raceline.edges_for(inner, closed),
+                                    outer_seg=raceline.edges_for(outer, closed), veh_width=0.6, closed=closed)))
+    N = 1500
+    t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+    k = np.linspace(0, 2 * np.pi, 1037, endpoint=False)
+    out.append(("dense", abi.Problem(
+        center=np.stack([30 * np.cos(t) + 3 * np.cos(3 * t), 18 * np.sin(t)], axis=1), L=1.0,
+        inner_seg=raceline.ring_edges(np.stack([27 * np.cos(k) + 3 * np.cos(3 * k), 15.5 * np.sin(k)], axis=1)),
+        outer_seg=raceline.ring_edges(np.stack([33 * np.cos(k) + 3 * np.cos(3 * k), 20.5 * np.sin(k)], axis=1)),
+        veh_width=1.0, closed=True)))
+    return out
+
+
+def test_corridor_vs_oracle():
+    """The corridor itself (rl_corridor: the optimiser's scan with block culling) equals
+    the oracle's safe_ray corridor (ref:692-711) bit for bit, zero signs included."""
+    _lib_or_skip()
+    cfg = abi.default_cfg()
+    for name, prob in _corridor_cases():
+        lo, hi = raceline.corridor(prob, cfg)
+        olo, ohi = O.run_oracle_corridor(prob, cfg)
+        for what, g, r in (("lo", lo, olo), ("hi", hi, ohi)):
+            bad = np.flatnonzero((g != r) | (np.signbit(g) != np.signbit(r)))
+            assert bad.size == 0, f"{name}.{what}: {bad.size} samples differ, first {bad[:5]} {g[bad[:3]]} vs {r[bad[:3]]}"
