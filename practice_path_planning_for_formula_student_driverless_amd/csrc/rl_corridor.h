@@ -218,9 +218,16 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
 // minDistanceToSegments_global (ref:501-512) for the samples with need[k], exact for
 // every sample whose minimum is <= rad[k] (md[k] = +inf or a value > rad[k] otherwise).
 // Lane-level filters per block and per entry: the samples' bounding circle (centre q0,
-// radius max_k rad[k] + |q_k - q0|_1) against the block circle, then against
-// |mid - q0| <= R + half_len.
-template <int CK>
+// radius max_k r_k + |q_k - q0|_1) against the block circle, then against
+// |mid - q0| <= r + half_len.  Two passes over the surviving entries:
+//   1. the nearest segment midpoint to q0, at distance m: a midpoint lies on its
+//      segment, so md_k <= m + |q_k - q0| and the search radius of sample k drops to
+//      r_k = min(rad_k, m + |q_k - q0|);
+//   2. the candidates within that radius, walked in entry order; a candidate whose
+//      lower bound |q_k - mid| - half_len already exceeds the running minimum md_k
+//      cannot lower it (std::min keeps the first of equal values), so only the others
+//      get the exact reference distance.
+template <int CK, bool TIGHT = true, bool PRUNE = true>
 __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
                                              const bool (&need)[CK], const double (&rad)[CK], double (&md)[CK]) {
     cdbl* SR = as_cdbl(R.rec);             // [M][8] SegRec fields (uniform reads)
@@ -228,15 +235,18 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
     cdbl* BK = as_cdbl(R.blk);
     const SegRec* __restrict__ S = R.rec;
     const double cx = qx[0], cy = qy[0];
+    double dk[CK];                         // |q_k - q0|_1, rounded up
     double Rl = -1.0;
     bool lneed = false;
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
         md[k] = INFINITY;
-        if (need[k]) Rl = fmax(Rl, rad[k] + (fabs(qx[k] - cx) + fabs(qy[k] - cy)) * (1.0 + 1e-12));
+        dk[k] = (fabs(qx[k] - cx) + fabs(qy[k] - cy)) * (1.0 + 1e-12);
+        if (need[k]) Rl = fmax(Rl, rad[k] + dk[k]);
         lneed |= need[k];
     }
-    for (int b0 = 0; b0 < R.M; b0 += 32) {
+    // blocks whose circle meets the search circle (wave-uniform mask of one word)
+    auto visit_of = [&](int b0) -> uint32_t {
         uint32_t visit = 0u;
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
@@ -246,6 +256,35 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
             const bool nb = lneed && rb >= 0.0 && !(dx * dx + dy * dy > r * r);
             if (__any(nb)) visit |= 1u << q;
         }
+        return visit;
+    };
+    // pass 1: nearest midpoint (padding and chain starts carry NaN mids: fmin skips them)
+    double m2 = INFINITY;
+    for (int b0 = 0; TIGHT && b0 < R.M; b0 += 32) {
+        const uint32_t visit = visit_of(b0);
+        if (visit == 0u) continue;
+#pragma unroll
+        for (int q = 0; q < 32 / RL_BLK; ++q) {
+            if (!((visit >> q) & 1u)) continue;
+#pragma unroll
+            for (int j = 0; j < RL_BLK; ++j) {
+                cdbl* sr = SR + 8 * (b0 + q * RL_BLK + j);
+                const double dx = cx - sr[5], dy = cy - sr[6];
+                m2 = fmin(m2, dx * dx + dy * dy);
+            }
+        }
+    }
+    if (isfinite(m2)) {
+        const double m = sqrt(m2) * (1.0 + 1e-12) + 1e-12;
+        double R2 = -1.0;
+#pragma unroll
+        for (int k = 0; k < CK; ++k)
+            if (need[k]) R2 = fmax(R2, fmin(rad[k], m + dk[k]) + dk[k]);
+        Rl = R2;
+    }
+    // pass 2: candidates and the exact distances
+    for (int b0 = 0; b0 < R.M; b0 += 32) {
+        const uint32_t visit = visit_of(b0);
         if (threadIdx.x % 64 == 0) { RL_CNT(4, 4); RL_CNT(5, __popc(visit)); }
         if (visit == 0u) continue;
         uint32_t w = 0u;
@@ -268,11 +307,17 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
             w &= ~(0x80000000u >> j);
             const SegRec* s = S + b0 + j;
             const double x0 = s->x0, y0 = s->y0, sx = s->vx, sy = s->vy, dn = s->denom;
+            const double mx = s->mx, my = s->my, hr = s->hr;
             if (threadIdx.x % 64 == 0) RL_CNT(6, 1);              // fallback walk iterations (wave)
-            if (h) RL_CNT(7, 1);                                  // exact distance evaluations (lane)
 #pragma unroll
-            for (int k = 0; k < CK; ++k)
-                if (h && need[k]) md[k] = smin(md[k], seg_dist_exact(x0, y0, sx, sy, dn, qx[k], qy[k]));
+            for (int k = 0; k < CK; ++k) {
+                const double ex = qx[k] - mx, ey = qy[k] - my, lim = md[k] + hr;
+                const bool may = h && need[k] && (!PRUNE || !(ex * ex + ey * ey > lim * lim));
+                if (may) {
+                    RL_CNT(7, 1);                                 // exact distance evaluations (lane)
+                    md[k] = smin(md[k], seg_dist_exact(x0, y0, sx, sy, dn, qx[k], qy[k]));
+                }
+            }
         }
     }
 }
@@ -300,7 +345,7 @@ __device__ __forceinline__ void ring_vertex_ub(const RingDesc& R, const double (
 // (std::min returns the same value on ties), so md_r is searched only within
 // rad = min(ub, s_max) and reported as +inf when it exceeds it.
 // Inactive samples (act false) do no exact work; the caller zeroes their outputs.
-template <int CK>
+template <int CK, bool TIGHT = true, bool PRUNE = true>
 __device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDesc& Ro, const double (&qx)[CK],
                                                 const double (&qy)[CK], const double (&ux)[CK],
                                                 const double (&uy)[CK], const bool (&act)[CK], double guard,
@@ -338,7 +383,7 @@ __device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDe
             const double lim = sqrt(ub2[r][k]) * (1.0 + 1e-9) + 1e-12;   // >= the true minimum
             rad[k] = fmin(lim, rad[k] * (1.0 + 1e-9) + 1e-12);
         }
-        ring_mindist<CK>(R, qx, qy, need, rad, md[r]);
+        ring_mindist<CK, TIGHT, PRUNE>(R, qx, qy, need, rad, md[r]);
     }
 #pragma unroll
     for (int k = 0; k < CK; ++k) {

@@ -46,6 +46,12 @@ namespace rl {
 #define RL_SPEC_GRAD 0   // 1: interior of the next gradient ahead of the reduction (A/B: slower)
 #endif
 constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per ring pass)
+#ifndef RL_MD_TIGHT
+#define RL_MD_TIGHT 0    // fallback search: nearest-midpoint radius pass (rl_corridor.h ring_mindist; A/B: +0.8% C2 here, -21% C5 in the streaming kernel)
+#endif
+#ifndef RL_MD_PRUNE
+#define RL_MD_PRUNE 1    // fallback search: running-minimum pruning in the exact walk
+#endif
 
 // Diagnostic build only (-DRL_STAMPS=1): per-phase s_memtime totals of each
 // workgroup's wave 0, written to a device array no other code reads.
@@ -384,7 +390,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                 act[k] = i0 + k < N;
             }
-            corridor_bounds<CKK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lc, hc);
+            corridor_bounds<CKK, RL_MD_TIGHT != 0, RL_MD_PRUNE != 0>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard,
+                                                                      lc, hc);
 #pragma unroll
             for (int k = 0; k < CKK; ++k) {
                 const int i = i0 + k;

@@ -138,15 +138,14 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
     double* __restrict__ V = sb.v + off;
     double* __restrict__ VS = sb.vs + off;
 
-    auto wrap = [&](int g) -> int {
-        if (CLOSED) { g %= N; if (g < 0) g += N; return g; }
-        return g < 0 ? 0 : (g >= N ? N - 1 : g);
-    };
+    // neighbour index i-1 / i+1: wrapped when closed, clamped when open (no integer division)
+    auto prev_i = [&](int i) -> int { return i > 0 ? i - 1 : (CLOSED ? N - 1 : 0); };
+    auto next_i = [&](int i) -> int { return i + 1 < N ? i + 1 : (CLOSED ? 0 : N - 1); };
     // deriv lambdas of ref:599-613 / 625-639 at sample i
     auto deriv = [&](int i, double& xp, double& yp, double& xpp, double& ypp) {
         if (N == 1) { xp = 1; yp = 0; xpp = ypp = 0; return; }
         if (CLOSED) {
-            const int ip = wrap(i + 1), im = wrap(i - 1);
+            const int ip = next_i(i), im = prev_i(i);
             xp = (X[ip] - X[im]) / two_h; yp = (Y[ip] - Y[im]) / two_h;
             xpp = (X[ip] - 2 * X[i] + X[im]) / hh; ypp = (Y[ip] - 2 * Y[i] + Y[im]) / hh;
         } else if (i == 0) {
@@ -166,7 +165,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
     auto normal_at = [&](int i) {
         double tx, ty;
         if (N == 1) { tx = 1; ty = 0; }
-        else if (CLOSED) { const int ip = wrap(i + 1), im = wrap(i - 1); tx = (X[ip] - X[im]) * 0.5; ty = (Y[ip] - Y[im]) * 0.5; }
+        else if (CLOSED) { const int ip = next_i(i), im = prev_i(i); tx = (X[ip] - X[im]) * 0.5; ty = (Y[ip] - Y[im]) * 0.5; }
         else if (i == 0) { tx = X[1] - X[0]; ty = Y[1] - Y[0]; }
         else if (i == N - 1) { tx = X[N - 1] - X[N - 2]; ty = Y[N - 1] - Y[N - 2]; }
         else { tx = (X[i + 1] - X[i - 1]) * 0.5; ty = (Y[i + 1] - Y[i - 1]) * 0.5; }
@@ -414,42 +413,82 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
         __syncthreads();
         RL_SSTAMP(3);
 
+        // the residual terms of sample i from the stencil values around it (ref:654-675 /
+        // 866-895): J term, Σa1² term, and q1, q2, D1α for the gradient
+        struct Term { double jz, x1, q1, q2; };
+        auto term_at = [&](int i, double am, double a0, double ap) -> Term {
+            const double x1 = d1_at(i, am, a0, ap), x2 = d2_at(i, am, a0, ap);
+            const double w = CW[i], A1 = CA1[i], A2 = CA2[i];
+            const double r = w * (CN0[i] + A1 * x1 + A2 * x2);
+            double jz, Wz;
+            if (MT) { const double g2 = G2[i]; jz = g2 * r * r; Wz = w * g2 * r; }
+            else { jz = r * r; Wz = w * r; }
+            return {jz, x1, A1 * Wz, A2 * Wz};
+        };
         // one evaluation of the vector `a` (already written and synchronised):
-        // J and the Armijo decrease; q1,q2,D1α to global for the gradient
-        auto eval_j = [&](const double* a, bool trial, double& dec) -> double {
+        // J; q1,q2,D1α to global for the gradient
+        auto eval_j = [&](const double* a) -> double {
+            double s3[2] = {0.0, 0.0};
+            for (int i = tid; i < N; i += TS) {
+                const Term t = term_at(i, a[prev_i(i)], a[i], a[next_i(i)]);
+                Q1[i] = t.q1;
+                Q2[i] = t.q2;
+                D1[i] = t.x1;
+                s3[0] += t.jz;
+                s3[1] += t.x1 * t.x1;
+            }
+            block_sum_s<2>(sm, s3, lane, wid);                     // two barriers: q/D1 visible after
+            return s3[0] + lam * s3[1];
+        };
+        // the trial vector of step st at sample j: std::min(hi, std::max(lo, α - st*g)) (ref:731)
+        auto trial_at = [&](int j, double st) -> double { return smin(HI[j], smax(LO[j], al_p[j] - st * GR[j])); };
+        // one evaluation of the trial vector of step st: J and the Armijo decrease
+        // Σ g(α_trial - α) (ref:733 / 1009). Each sample recomputes its neighbours' trial
+        // values from (α, g, lo, hi), so a rejected trial writes nothing; `keep` also
+        // stores α_trial, q1, q2 and D1α, which an accepted step needs.
+        auto eval_trial = [&](double st, bool keep, double& dec) -> double {
             double s3[3] = {0.0, 0.0, 0.0};
             for (int i = tid; i < N; i += TS) {
-                const double am = a[wrap(i - 1)], a0 = a[i], ap = a[wrap(i + 1)];
-                const double x1 = d1_at(i, am, a0, ap), x2 = d2_at(i, am, a0, ap);
-                const double w = CW[i], A1 = CA1[i], A2 = CA2[i];
-                const double r = w * (CN0[i] + A1 * x1 + A2 * x2);
-                double jz, Wz;
-                if (MT) { const double g2 = G2[i]; jz = g2 * r * r; Wz = w * g2 * r; }
-                else { jz = r * r; Wz = w * r; }
-                Q1[i] = A1 * Wz;
-                Q2[i] = A2 * Wz;
-                D1[i] = x1;
-                s3[0] += jz;
-                s3[1] += x1 * x1;
-                if (trial) s3[2] += GR[i] * (a0 - al_p[i]);
+                const int im = prev_i(i), ip = next_i(i);
+                const double a0 = trial_at(i, st);
+                const double am = (im == i) ? a0 : trial_at(im, st);
+                const double ap = (ip == i) ? a0 : trial_at(ip, st);
+                const Term t = term_at(i, am, a0, ap);
+                if (keep) { an_p[i] = a0; Q1[i] = t.q1; Q2[i] = t.q2; D1[i] = t.x1; }
+                s3[0] += t.jz;
+                s3[1] += t.x1 * t.x1;
+                s3[2] += GR[i] * (a0 - al_p[i]);
             }
-            block_sum_s<3>(sm, s3, lane, wid);                     // two barriers: q/D1 visible after
+            block_sum_s<3>(sm, s3, lane, wid);                     // two barriers: writes visible after
             dec = s3[2];
             return s3[0] + lam * s3[1];
         };
+        // an accepted trial that was evaluated without `keep`: write what it would have
+        auto materialize = [&](double st) {
+            for (int i = tid; i < N; i += TS) {
+                const int im = prev_i(i), ip = next_i(i);
+                const double a0 = trial_at(i, st);
+                const double am = (im == i) ? a0 : trial_at(im, st);
+                const double ap = (ip == i) ? a0 : trial_at(ip, st);
+                const Term t = term_at(i, am, a0, ap);
+                an_p[i] = a0; Q1[i] = t.q1; Q2[i] = t.q2; D1[i] = t.x1;
+            }
+            __syncthreads();
+        };
         auto eval_grad = [&]() {
             for (int i = tid; i < N; i += TS) {
-                const int im = wrap(i - 1), ip = wrap(i + 1);
+                const int im = prev_i(i), ip = next_i(i);
                 const double g1 = d1t_at(i, Q1[im], Q1[i], Q1[ip]);
                 const double g2 = d2t_at(i, Q2[im], Q2[i], Q2[ip]);
                 const double gsm = d1t_at(i, D1[im], D1[i], D1[ip]);
                 GR[i] = 2.0 * (g1 + g2) + lam2 * gsm;
             }
+            __syncthreads();                                       // the next trial reads g at i±1
         };
 
         double step = C.step_init;
         double dec;
-        double J = eval_j(al_p, false, dec);
+        double J = eval_j(al_p);
         eval_grad();
         int evals = 1, accepts = 0;
         double J_prev = J;
@@ -457,14 +496,13 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
-                for (int i = tid; i < N; i += TS) an_p[i] = smin(HI[i], smax(LO[i], al_p[i] - step * GR[i]));   // std:: semantics (ref:731)
-                __syncthreads();
-#ifdef RL_EXP_EVAL2
-                (void)eval_j(an_p, true, dec);
-#endif
-                const double Jn = eval_j(an_p, true, dec);
+                // the first trial of an inner iteration is the usual accept: keep its
+                // vectors; later (backtracked) trials are mostly rejected
+                const bool keep = (bt == 0);
+                const double Jn = eval_trial(step, keep, dec);
                 ++evals;
                 if (Jn <= J + C.armijo_c * dec) {
+                    if (!keep) materialize(step);
                     double* t = al_p; al_p = an_p; an_p = t;       // α := α_trial (uniform swap)
                     eval_grad();
                     J = Jn;

@@ -6,7 +6,7 @@ rev=${1:-HEAD}
 repo=$(cd "$(dirname "$0")/.." && pwd)
 pkg=practice_path_planning_for_formula_student_driverless_amd
 vdir=$repo/$pkg/_lib/variants
-rm -rf "$vdir"; mkdir -p "$vdir"
+mkdir -p "$vdir"; rm -f "$vdir/librl_base.so" "$vdir/librl_new.so"
 tmp=$(mktemp -d)
 git -C "$repo" archive "$rev" $pkg/csrc include | tar -x -C "$tmp"
 python3 - "$repo" "$tmp" "$vdir" <<'PY'
