@@ -542,24 +542,39 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
         if (j <= N - 2) acc += ((j + 1 == N - 1) ? -invh : -inv2h) * vp;
         return acc;
     };
-    auto d2t_at = [&](int k, double vm, double v0, double vp) RL_AI -> double {  // D2T ref:558 / 576-578
-        if (CLOSED) return (vp - 2 * v0 + vm) * invh2;
+
+    // gradient at own sample k from the stencil inputs around it (ref:668-673 / 886-893):
+    // 2.0*(g1+g2) + lam2*gsm. Scaling by 2 is exact, so 2*(g1+g2) = 2*g1 + 2*g2 and
+    // 2*g1 = D1T(q1) with the coefficients doubled (likewise D2T(q2)), bit for bit as
+    // long as no product is subnormal: the factor 2 costs no multiplication.
+    const double inv2h_x2 = 2.0 * inv2h, invh_x2 = 2.0 * invh, invh2_x2 = 2.0 * invh2, m2invh2_x2 = 2.0 * m2invh2;
+    auto d1t_x2 = [&](int k, double vm, double v0, double vp) RL_AI -> double {   // 2*D1T (ref:555-557 / 567-572)
+        if (CLOSED) return (vm - vp) * inv2h_x2;
+        const int j = base + k;
+        if (N <= 1) return 0.0;
+        double acc = 0.0;
+        if (j >= 1) acc += ((j == 1) ? invh_x2 : inv2h_x2) * vm;
+        if (j == 0) acc += (-invh_x2) * v0;
+        else if (j == N - 1) acc += (+invh_x2) * v0;
+        if (j <= N - 2) acc += ((j + 1 == N - 1) ? -invh_x2 : -inv2h_x2) * vp;
+        return acc;
+    };
+    auto d2t_x2 = [&](int k, double vm, double v0, double vp) RL_AI -> double {   // 2*D2T (ref:558 / 576-578)
+        if (CLOSED) return (vp - 2 * v0 + vm) * invh2_x2;
         const int j = base + k;
         if (N <= 2) return 0.0;
         double acc = 0.0;
-        if (j - 1 >= 1 && j - 1 <= N - 2) acc += (+invh2) * vm;
-        if (j >= 1 && j <= N - 2) acc += m2invh2 * v0;
-        if (j + 1 >= 1 && j + 1 <= N - 2) acc += (+invh2) * vp;
+        if (j - 1 >= 1 && j - 1 <= N - 2) acc += (+invh2_x2) * vm;
+        if (j >= 1 && j <= N - 2) acc += m2invh2_x2 * v0;
+        if (j + 1 >= 1 && j + 1 <= N - 2) acc += (+invh2_x2) * vp;
         return acc;
     };
-
-    // gradient at own sample k from the stencil inputs around it (ref:668-673 / 886-893)
     auto grad_at = [&](int k, double q1m, double q10, double q1p, double q2m, double q20, double q2p, double am,
                        double a0, double ap) RL_AI -> double {
-        double g1 = d1t_at(k, q1m, q10, q1p);
-        double g2 = d2t_at(k, q2m, q20, q2p);
+        double g1 = d1t_x2(k, q1m, q10, q1p);
+        double g2 = d2t_x2(k, q2m, q20, q2p);
         double gsm = d1t_at(k, am, a0, ap);
-        return 2.0 * (g1 + g2) + lam2 * gsm;
+        return (g1 + g2) + lam2 * gsm;
     };
 
     // ---- state ------------------------------------------------------------
