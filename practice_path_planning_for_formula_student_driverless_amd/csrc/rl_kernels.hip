@@ -272,6 +272,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     // ---- neighbour exchange (DPP in-wave, LDS across waves and for the wrap) ----
     // before a barrier: the wave's edge values (and the wrap value) go to LDS
     auto xpub = [&](int slot, const double (&a)[K]) RL_AI {
+        if constexpr (NW == 1) return;       // one wave: xget reads the edges with readlane
         const double first = a[0], last = a[K - 1];
         *((lane == 0) ? &sm.eF[slot][wid] : &sm.sink[lane]) = first;
         *((lane == 63) ? &sm.eL[slot][wid] : &sm.sink[lane]) = last;
@@ -285,15 +286,24 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
     // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped).
     // In-wave neighbours by DPP; lanes 0 / 63 keep the other wave's edge value.
     auto xget = [&](int slot, const double (&a)[K], double& lv, double& rv) RL_AI {
-        const double el = (wid > 0) ? sm.eL[slot][(wid > 0) ? wid - 1 : 0] : sm.wL[slot];   // wave-uniform reads
-        const double ef = sm.eF[slot][(wid + 1 < NW) ? wid + 1 : 0];
+        double el, ef;
+        if constexpr (NW == 1) {
+            // the same values as the LDS tables hold: the last valid value of the last
+            // active thread (closed wrap) and lane 0's first value
+            const double lastv = (!RAGGED || cntL == K) ? a[K - 1] : pick(a, cnt - 1);
+            el = readlane(lastv, Ta - 1);
+            ef = readlane(a[0], 0);
+        } else {
+            el = (wid > 0) ? sm.eL[slot][(wid > 0) ? wid - 1 : 0] : sm.wL[slot];   // wave-uniform reads
+            ef = sm.eF[slot][(wid + 1 < NW) ? wid + 1 : 0];
+        }
         lv = dpp_from_left_or(a[K - 1], el);
         rv = dpp_from_right_or(a[0], ef);
         // the closed wrap for the last active thread; inactive lanes keep whatever
         // their neighbours hold (finite) -- their coefficients and bounds are zero,
         // so only their Σa1² term could leak, and lam_act removes it
         if (CLOSED && tail_wave) {
-            const double e0 = sm.eF[slot][0];
+            const double e0 = (NW == 1) ? ef : sm.eF[slot][0];
             if (is_last) rv = e0;
         }
     };
@@ -603,7 +613,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
             }
         }
         xpub(0, a);
-        __syncthreads();
+        if constexpr (NW > 1) __syncthreads();
 #ifdef RL_EXP_BAR      // experiment: one extra barrier per evaluation (cost probe)
         __syncthreads();
 #endif
@@ -668,6 +678,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel
 #if RL_MFMA_RED
         if (trial) pdec = wave_sum_mfma(pdec);
 #endif
+        if constexpr (NW == 1) {             // the wave sums are the block sums
+            dec = pdec;
+            return pJ;
+        }
         if (lane == 0) { sm.red[0][wid] = pJ; sm.red[2][wid] = pdec; }
         __syncthreads();
         double J = sm.red[0][0], D = sm.red[2][0];
