@@ -214,7 +214,7 @@ template <int K, int T>
 struct MinWaves {
     static constexpr int value = (K == RL_MID_K && T == RL_MID_T)       ? RL_MID_W
                                  : (K == RL_MIDMT_K && T == RL_MIDMT_T) ? RL_MIDMT_W
-                                 : ((T >= 512) ? 1 : (T == 64 ? 4 : 2));
+                                 : ((T >= 512) ? 1 : ((T == 64 && K == 4) ? 4 : 2));
 };
 
 // RAGGED: N % K != 0, i.e. one thread holds a partial chunk (decided per launch; the
@@ -985,6 +985,7 @@ static hipError_t launch_ktm(const KParams& p, hipStream_t st) {
 
 // variant table by N: (K samples per lane, T lanes per instance)
 //   N <= 256          (4, 64)      one wave per instance
+//   N <= 512          (8, 64)      one wave per instance
 //   N <= 1024         (8, 128)
 //   N <= 2048         (RL_MID_K, RL_MID_T)   default (8, 256); min-time (RL_MIDMT_K, RL_MIDMT_T) = (4, 512)
 //   N <= 4096         (8, 512)
@@ -992,6 +993,7 @@ static_assert(RL_MID_K * RL_MID_T == 2048, "mid variant must cover N <= 2048");
 static_assert(RL_MIDMT_K * RL_MIDMT_T == 2048, "mid min-time variant must cover N <= 2048");
 int pick_k(int N) {
     if (N <= 4 * 64) return 4;
+    if (N <= 8 * 64) return 8;
     if (N <= 8 * 128) return 8;
     if (N <= 2048) return RL_MID_K;
     if (N <= 8 * 512) return 8;
@@ -1001,6 +1003,7 @@ int pick_k(int N) {
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
     if (p.N <= 4 * 64) return launch_kt<4, 64>(p, mintime, st);
+    if (p.N <= 8 * 64) return launch_kt<8, 64>(p, mintime, st);      // one wave (single-wave paths)
     if (p.N <= 8 * 128) return launch_kt<8, 128>(p, mintime, st);
     if (p.N <= 2048)
         return mintime ? launch_ktm<RL_MIDMT_K, RL_MIDMT_T, true>(p, st) : launch_ktm<RL_MID_K, RL_MID_T, false>(p, st);
