@@ -209,18 +209,46 @@ struct alignas(16) Smem {
 #define RL_MIDMT_W 2
 #endif
 
+// single-wave (4, 64) variant (N <= 256: the bundled tracks, C1/C4) per mode.  A/B on
+// C4-shaped plans (scripts/ab_c4.py, kernel-time sum): 4 waves/SIMD (128 VGPRs) spilled
+// 148 B/lane (min-curv) and 596 B/lane (min-time); 2 waves/SIMD: 61.9 -> 51.1 ms
+#ifndef RL_SMALL_W
+#define RL_SMALL_W 2
+#endif
+#ifndef RL_SMALLMT_W
+#define RL_SMALLMT_W 2
+#endif
+// (8, 64) (256 < N <= 512) and (8, 128) (512 < N <= 1024) per mode; (8, 64) min-time
+// spills 540 B/lane at 2 waves/SIMD, 1 wave/SIMD lets it use the AGPRs (C4: -2.5%)
+#ifndef RL_S8_W
+#define RL_S8_W 2
+#endif
+#ifndef RL_S8MT_W
+#define RL_S8MT_W 1
+#endif
+#ifndef RL_M8_W
+#define RL_M8_W 2
+#endif
+#ifndef RL_M8MT_W
+#define RL_M8MT_W 2
+#endif
+
 // waves per SIMD to keep resident (caps the register budget the compiler may use)
-template <int K, int T>
+template <int K, int T, bool MT>
 struct MinWaves {
     static constexpr int value = (K == RL_MID_K && T == RL_MID_T)       ? RL_MID_W
                                  : (K == RL_MIDMT_K && T == RL_MIDMT_T) ? RL_MIDMT_W
-                                 : ((T >= 512) ? 1 : ((T == 64 && K == 4) ? 4 : 2));
+                                 : (T >= 512)                           ? 1
+                                 : (T == 64 && K == 4)                  ? (MT ? RL_SMALLMT_W : RL_SMALL_W)
+                                 : (T == 64 && K == 8)                  ? (MT ? RL_S8MT_W : RL_S8_W)
+                                 : (T == 128 && K == 8)                 ? (MT ? RL_M8MT_W : RL_M8_W)
+                                                                        : 2;
 };
 
 // RAGGED: N % K != 0, i.e. one thread holds a partial chunk (decided per launch; the
 // exact-multiple version carries no partial-chunk bookkeeping)
 template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
-__global__ __launch_bounds__(T, (MinWaves<K, T>::value)) void rl_optimize_kernel(KParams p) {
+__global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_kernel(KParams p) {
     constexpr int NW = T / 64;
     __shared__ Smem<K, T> sm;
 #ifdef RL_STAMPS

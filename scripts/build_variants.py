@@ -13,6 +13,11 @@ VARIANTS = {
     "exp_corr2": {"RL_EXP_CORR2": 1},
     "exp_bar": {"RL_EXP_BAR": 1},
     "exp_red": {"RL_EXP_RED": 1},
+    "old_w": {"RL_SMALLMT_W": 4, "RL_SMALL_W": 4, "RL_S8MT_W": 2},   # before the per-mode occupancy A/B
+    "smc_w4": {"RL_SMALL_W": 4},
+    "smc_w3": {"RL_SMALL_W": 3},
+    "smt_w3": {"RL_SMALLMT_W": 3},
+    "s8mt_w2": {"RL_S8MT_W": 2},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
 }
 if __name__ == "__main__":
