@@ -1016,6 +1016,7 @@ static hipError_t launch_ktm(const KParams& p, hipStream_t st) {
 //   N <= 512          (8, 64)      one wave per instance
 //   N <= 1024         (8, 128)
 //   N <= 2048         (RL_MID_K, RL_MID_T)   default (8, 256); min-time (RL_MIDMT_K, RL_MIDMT_T) = (4, 512)
+//                     below two instances per CU, else (RL_MID_K, RL_MID_T)
 //   N <= 4096         (8, 512)
 static_assert(RL_MID_K * RL_MID_T == 2048, "mid variant must cover N <= 2048");
 static_assert(RL_MIDMT_K * RL_MIDMT_T == 2048, "mid min-time variant must cover N <= 2048");
@@ -1028,13 +1029,32 @@ int pick_k(int N) {
     return -1;
 }
 
+#ifndef RL_MIDMT_BIG
+#define RL_MIDMT_BIG 1
+#endif
+static int cu_count() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 256;
+    return n > 0 ? n : 256;
+}
+
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
     if (p.N <= 4 * 64) return launch_kt<4, 64>(p, mintime, st);
     if (p.N <= 8 * 64) return launch_kt<8, 64>(p, mintime, st);      // one wave (single-wave paths)
     if (p.N <= 8 * 128) return launch_kt<8, 128>(p, mintime, st);
-    if (p.N <= 2048)
-        return mintime ? launch_ktm<RL_MIDMT_K, RL_MIDMT_T, true>(p, st) : launch_ktm<RL_MID_K, RL_MID_T, false>(p, st);
+    if (p.N <= 2048) {
+        if (!mintime) return launch_ktm<RL_MID_K, RL_MID_T, false>(p, st);
+#if RL_MIDMT_BIG
+        // min-time: (4, 512) holds one instance per CU (8 waves at 2 waves/SIMD), the
+        // lower latency while the batch leaves CUs idle; from two instances per CU up,
+        // the (RL_MID_K, RL_MID_T) shape keeps two per CU resident for throughput
+        if (p.B >= 2 * cu_count()) return launch_ktm<RL_MID_K, RL_MID_T, true>(p, st);
+#endif
+        return launch_ktm<RL_MIDMT_K, RL_MIDMT_T, true>(p, st);
+    }
     return launch_kt<8, 512>(p, mintime, st);
 }
 

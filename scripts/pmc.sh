@@ -5,7 +5,7 @@
 out=${1:-gpurun_out/pmc}
 mkdir -p "$out"
 export TMPDIR=/tmp
-cmd="python bench.py --steps 2 --warmup 0 --no-cpu --no-extras"
+cmd=${PMC_CMD:-"python bench.py --steps 2 --warmup 0 --no-cpu --no-extras"}
 passes=(
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
   "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SMEM SQ_WAIT_INST_LDS"

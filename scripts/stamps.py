@@ -21,3 +21,11 @@ for cname, B, modes in (("cmap1_n2000", 1024, 1), ("cmap1_n2000_vp20", 256, 2)):
     for i, nm in enumerate(names):
         if tot[i] > 0: print(f"   {nm:18s} {100*tot[i]/tot.sum():5.1f}%")
     lib.rl_plan_destroy(h)
+# evaluations per outer iteration of the C3 min-curv / min-time runs (main library)
+from practice_path_planning_for_formula_student_driverless_amd import raceline
+case = O.load_case("cmap1_n2000_vp20"); prob = O.case_problem(case); cfg = O.case_cfg(case)
+pl = raceline.Plan(prob, cfg, seeds=np.arange(256, dtype=np.uint64), B=256, modes=3)
+pl.run(); mc, mt = pl.fetch()
+print(f"C3 evals/outer: min-curv {mc.evals.mean():.2f}, min-time {mt.evals.mean():.2f}; "
+      f"kernel ms {pl.kernel_ms(1):.2f} / {pl.kernel_ms(2):.2f}")
+pl.close()

@@ -133,6 +133,35 @@ def test_n2000_seeds_vs_oracle():
     compare_outputs(mt, omt, True, "n2000.mt")
 
 
+def _pick_rows(o: abi.Outputs, rows, mintime: bool) -> abi.Outputs:
+    kw = {f: getattr(o, f)[rows] for f in abi.OUT_F64 + ("evals", "accepts")}
+    if mintime:
+        kw.update(v=o.v[rows], ax=o.ax[rows], lap=o.lap[rows], vpass_sweeps=o.vpass_sweeps[rows])
+    return abi.Outputs(**kw)
+
+
+@pytest.mark.parametrize("closed", [True, False])
+def test_n2000_mintime_throughput_shape(closed):
+    """From two instances per CU up (B >= 512 on MI355X), min-time at 1024 < N <= 2048
+    runs the (8, 256) shape instead of (4, 512): against the oracle on three seeds, and
+    the small-batch run's columns bit for bit (the lap sum's tree order may differ)."""
+    _lib_or_skip()
+    case = O.load_case("cmap1_n2000_vp20")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    if not closed:
+        prob = _synthetic(2047, False, np.random.default_rng(7))
+    B = 512
+    seeds = np.arange(B, dtype=np.uint64)
+    _, mt = raceline.optimize_batch(prob, cfg, seeds, B, mincurv=False, mintime=True)
+    pick = np.array([0, 5, 6])
+    _, omt = O.run_oracle(prob, cfg, seeds=seeds[pick], B=len(pick), modes=(False, True))
+    compare_outputs(_pick_rows(mt, pick, True), omt, True, "n2000big.mt")
+    _, smt = raceline.optimize_batch(prob, cfg, seeds[pick], len(pick), mincurv=False, mintime=True)
+    for f in abi.OUT_F64 + ("v", "ax", "evals", "accepts", "vpass_sweeps"):
+        np.testing.assert_array_equal(getattr(mt, f)[pick], getattr(smt, f), err_msg=f"big vs small shape: {f}")
+    np.testing.assert_allclose(mt.lap[pick], smt.lap, rtol=1e-13, atol=0)
+
+
 def _synthetic(N, closed, rng):
     t = np.linspace(0, 2 * np.pi, N, endpoint=False)
     r = 20 + rng.uniform(-0.05, 0.05, N)
