@@ -186,6 +186,9 @@ def run_c5(world, rank, local, dev, dist):
             "outer_iters_per_s": round(world * B * 14 / (k_ms * 1e-3), 1), "evals_per_outer": E_k,
             "roofline": {"bound": "hbm", "achieved": round(by / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(by / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": read_pmc("c5_mincurv"),
+                         "measured_hbm_GBps": (round(read_pmc("c5_mincurv") / (k_ms * 1e-3) / 1e9, 1)
+                                               if read_pmc("c5_mincurv") else None),
                          "model": "SURVEY §8d streaming bytes N*(80*E_k+224)+32*E per outer"},
             "seed0_vs_reference_max_rel_err": rel}
 

@@ -52,8 +52,15 @@ __device__ __forceinline__ double wave_sum_s(double x) {
     return (readlane_s(x, 0) + readlane_s(x, 16)) + (readlane_s(x, 32) + readlane_s(x, 48));
 }
 
+// backtracking trials evaluated per pass over the state once the first trial of an
+// inner iteration is rejected (min-curv; min-time keeps one per pass)
+#ifndef RL_BT_BATCH
+#define RL_BT_BATCH 4
+#endif
+constexpr int RED_SLOTS = 3 * RL_BT_BATCH > 4 ? 3 * RL_BT_BATCH : 4;
+
 struct SSmem {
-    double red[4][NWS];
+    double red[RED_SLOTS][NWS];
     double vin[2][TS];
     double bc[4];
 };
@@ -486,6 +493,41 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             __syncthreads();                                       // the next trial reads g at i±1
         };
 
+        // The next up-to-MB steps of a backtracking run (C5: every trial of an outer
+        // iteration is rejected) from one pass over (α, g, lo, hi, coefficients): per
+        // step the arithmetic and the per-thread sample order of eval_trial, and
+        // block_sum_s reduces each sum on its own, so J and the decrease of every step
+        // are bit-identical to one-at-a-time trials.  Writes nothing.
+        constexpr int MB = MT ? 1 : RL_BT_BATCH;
+        auto eval_trials = [&](const double (&st)[MB], int m, double (&Jn)[MB], double (&dn)[MB]) {
+            double s3[3 * MB];
+#pragma unroll
+            for (int j = 0; j < 3 * MB; ++j) s3[j] = 0.0;
+            for (int i = tid; i < N; i += TS) {
+                const int im = prev_i(i), ip = next_i(i);
+                const double a0v = al_p[i], g0 = GR[i], lo0 = LO[i], hi0 = HI[i];
+                const double amv = al_p[im], gm = GR[im], lom = LO[im], him = HI[im];
+                const double apv = al_p[ip], gp = GR[ip], lop = LO[ip], hip = HI[ip];
+                const double w = CW[i], A1 = CA1[i], A2 = CA2[i], n0 = CN0[i];
+#pragma unroll
+                for (int j = 0; j < MB; ++j) {
+                    if (j < m) {                                      // uniform
+                        const double a0 = smin(hi0, smax(lo0, a0v - st[j] * g0));
+                        const double am = (im == i) ? a0 : smin(him, smax(lom, amv - st[j] * gm));
+                        const double ap = (ip == i) ? a0 : smin(hip, smax(lop, apv - st[j] * gp));
+                        const double x1 = d1_at(i, am, a0, ap), x2 = d2_at(i, am, a0, ap);
+                        const double r = w * (n0 + A1 * x1 + A2 * x2);
+                        s3[3 * j] += r * r;
+                        s3[3 * j + 1] += x1 * x1;
+                        s3[3 * j + 2] += g0 * (a0 - a0v);
+                    }
+                }
+            }
+            block_sum_s<3 * MB>(sm, s3, lane, wid);
+#pragma unroll
+            for (int j = 0; j < MB; ++j) { Jn[j] = s3[3 * j] + lam * s3[3 * j + 1]; dn[j] = s3[3 * j + 2]; }
+        };
+
         double step = C.step_init;
         double dec;
         double J = eval_j(al_p);
@@ -496,6 +538,39 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
+                if (MB > 1 && bt > 0) {
+                    // the steps ref:737-740 would try next: halve, stop at 20 backtracks
+                    // or below step_min
+                    double st[MB], Jn[MB], dn[MB];
+                    int m = 1;
+                    st[0] = step;
+#pragma unroll
+                    for (int j = 1; j < MB; ++j) {
+                        const double sj = st[j - 1] * 0.5;
+                        st[j] = sj;
+                        if (m == j && bt + j < 20 && !(sj < C.step_min)) m = j + 1;
+                    }
+                    eval_trials(st, m, Jn, dn);
+                    bool stop = false;
+                    for (int j = 0; j < m; ++j) {
+                        ++evals;
+                        if (Jn[j] <= J + C.armijo_c * dn[j]) {
+                            materialize(st[j]);
+                            double* t = al_p; al_p = an_p; an_p = t;
+                            eval_grad();
+                            J = Jn[j];
+                            accepted = true;
+                            ++accepts;
+                            stop = true;
+                            break;
+                        }
+                        step *= 0.5;
+                        bt++;
+                        if (step < C.step_min) { stop = true; break; }
+                    }
+                    if (stop) break;
+                    continue;
+                }
                 // the first trial of an inner iteration is the usual accept: keep its
                 // vectors; later (backtracked) trials are mostly rejected
                 const bool keep = (bt == 0);

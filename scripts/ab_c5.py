@@ -28,3 +28,13 @@ for r in range(4):
         times[n].append(ms.value)
 for n, t in times.items():
     print(f"C5 B={B} modes={modes} {n:12s} median {np.median(t[1:]):8.2f} ms  min {min(t[1:]):8.2f}", flush=True)
+outs = {}
+for n, (lib, h) in plans.items():
+    o = abi.Outputs.alloc(B, prob.N, 14, modes == 2)
+    c = o.as_c()
+    lib.rl_plan_fetch(h, C.byref(c), None) if modes == 1 else lib.rl_plan_fetch(h, None, C.byref(c))
+    outs[n] = o
+base = next(iter(libs))
+for n in libs:
+    same = all(np.array_equal(getattr(outs[n], f), getattr(outs[base], f)) for f in ("x", "y", "alpha_last", "kappa", "evals", "accepts"))
+    print(f"C5 {n:12s} bitexact_vs_{base}: {same}; evals/outer {outs[n].evals.mean():.2f}", flush=True)

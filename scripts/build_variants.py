@@ -18,6 +18,9 @@ VARIANTS = {
     "smc_w3": {"RL_SMALL_W": 3},
     "smt_w3": {"RL_SMALLMT_W": 3},
     "s8mt_w2": {"RL_S8MT_W": 2},
+    "bt1": {"RL_BT_BATCH": 1},
+    "bt6": {"RL_BT_BATCH": 6},
+    "bt8": {"RL_BT_BATCH": 8},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
 }
 if __name__ == "__main__":

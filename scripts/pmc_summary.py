@@ -60,7 +60,8 @@ print(json.dumps(res, indent=1))
 if "--commit" in sys.argv and "hbm_bytes_per_launch" in der:
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     d = json.load(open(p)) if os.path.exists(p) else {}
-    d["c2_mincurv"] = {"hbm_bytes_per_launch": der["hbm_bytes_per_launch"], "fetch_bytes_raw": der["fetch_bytes_raw"],
+    key = sys.argv[sys.argv.index("--key") + 1] if "--key" in sys.argv else "c2_mincurv"
+    d[key] = {"hbm_bytes_per_launch": der["hbm_bytes_per_launch"], "fetch_bytes_raw": der["fetch_bytes_raw"],
                        "write_bytes": der["write_bytes"], "kernel": meta.get("kernel"), "source": out,
                        "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
                        "note": "rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate --pmc passes"}
