@@ -189,7 +189,10 @@ def run_c5(world, rank, local, dev, dist):
                          "traffic": read_pmc("c5_mincurv"),
                          "measured_hbm_GBps": (round(read_pmc("c5_mincurv") / (k_ms * 1e-3) / 1e9, 1)
                                                if read_pmc("c5_mincurv") else None),
-                         "model": "SURVEY §8d streaming bytes N*(80*E_k+224)+32*E per outer"},
+                         "model": "SURVEY §8d streaming bytes N*(80*E_k+224)+32*E per outer",
+                         "note": "frac > 1 is possible: batched backtracking reads the state once per 4 trial "
+                                 "steps, below the one-pass-per-evaluation model; measured_hbm_GBps is the "
+                                 "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE rate"},
             "seed0_vs_reference_max_rel_err": rel}
 
 

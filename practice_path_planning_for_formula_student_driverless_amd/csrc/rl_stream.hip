@@ -54,6 +54,11 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 
 // backtracking trials evaluated per pass over the state once the first trial of an
 // inner iteration is rejected (min-curv; min-time keeps one per pass)
+// corridor samples per lane in the streaming kernel (C5 A/B: 1 -> 36.0 ms, 2 -> 32.4 ms,
+// 4 -> 41.6 ms; scripts/ab_c5.py)
+#ifndef RL_SCK
+#define RL_SCK 2
+#endif
 #ifndef RL_BT_BATCH
 #define RL_BT_BATCH 4
 #endif
@@ -342,6 +347,30 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
             __syncthreads();
             RL_SSTAMP(6);
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
+#if RL_SCK > 1
+            // RL_SCK adjacent samples per lane (a wave scans 64*RL_SCK consecutive rays)
+            for (int i0 = RL_SCK * tid; i0 < N; i0 += RL_SCK * TS) {
+                double qx[RL_SCK], qy[RL_SCK], ux[RL_SCK], uy[RL_SCK], lk[RL_SCK], hk[RL_SCK];
+                bool act[RL_SCK];
+#pragma unroll
+                for (int k = 0; k < RL_SCK; ++k) {
+                    const int i = min(i0 + k, N - 1);
+                    qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
+                    act[k] = i0 + k < N;
+                }
+                corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
+#pragma unroll
+                for (int k = 0; k < RL_SCK; ++k) {
+                    const int i = i0 + k;
+                    if (act[k]) {
+                        HI[i] = hk[k];
+                        LO[i] = lk[k];
+                        if (outer == 0 && seed != 0)
+                            al_p[i] = smin(hk[k], smax(lk[k], seed_value(seed, i, RL_SEED_SIGMA)));
+                    }
+                }
+            }
+#else
             for (int i = tid; i < N; i += TS) {
 #ifdef RL_EXP_CORR2
                 corridor_at(i, guard);
@@ -350,6 +379,7 @@ __global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs s
                 if (outer == 0 && seed != 0)
                     al_p[i] = smin(HI[i], smax(LO[i], seed_value(seed, i, RL_SEED_SIGMA)));
             }
+#endif
         }
 #ifdef RL_STAMPS
         __syncthreads();

@@ -21,6 +21,8 @@ VARIANTS = {
     "bt1": {"RL_BT_BATCH": 1},
     "bt6": {"RL_BT_BATCH": 6},
     "bt8": {"RL_BT_BATCH": 8},
+    "sck1": {"RL_SCK": 1},
+    "sck4": {"RL_SCK": 4},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
 }
 if __name__ == "__main__":
