@@ -30,7 +30,12 @@
 namespace rl {
 
 namespace {
-constexpr int TS = 1024;          // threads per instance
+// threads per instance (C5 A/B: 1024 -> 32.5 ms, 512 -> 38.3 ms, 256 -> 36.7 ms;
+// profiles/r01/ab_c5_stream_wg.log)
+#ifndef RL_STS
+#define RL_STS 1024
+#endif
+constexpr int TS = RL_STS;        // threads per instance
 constexpr int NWS = TS / 64;
 
 template <int CTRL>
@@ -106,7 +111,7 @@ __device__ unsigned long long rl_dbg_stamps_s[16384][8];
 #endif
 
 template <bool CLOSED, bool MT>
-__global__ __launch_bounds__(1024) void rl_stream_kernel(KParams p, StreamBufs sb) {
+__global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb) {
     __shared__ SSmem sm;
 #ifdef RL_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -23,6 +23,8 @@ VARIANTS = {
     "bt8": {"RL_BT_BATCH": 8},
     "sck1": {"RL_SCK": 1},
     "sck4": {"RL_SCK": 4},
+    "sts512": {"RL_STS": 512},
+    "sts256": {"RL_STS": 256},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
 }
 if __name__ == "__main__":
