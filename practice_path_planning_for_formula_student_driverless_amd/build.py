@@ -46,10 +46,23 @@ def build_lib(force: bool = False) -> str:
     out = os.path.join(LIB_DIR, "librl.so")
     deps = KERNEL_DEPS + [os.path.join(INCLUDE, "rl_abi.h")]
     if force or _stale(out, deps):
-        tmp = out + ".tmp"
-        _run([HIPCC, *HIP_FLAGS, "-shared", *KERNEL_SRCS, "-o", tmp], cwd=PKG)
-        os.replace(tmp, out)
+        _compile_link(KERNEL_SRCS, [], out, os.path.join(LIB_DIR, "obj"))
     return out
+
+
+def _compile_link(srcs, flags, out, objdir) -> None:
+    """One hipcc process per translation unit (in parallel), then one link: the
+    kernel file alone takes ~100 s, so the others compile beside it."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
+    with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
+        for f in [ex.submit(_run, [HIPCC, *HIP_FLAGS, *flags, "-c", s, "-o", o], PKG) for s, o in zip(srcs, objs)]:
+            f.result()
+    tmp = out + ".tmp"
+    _run([HIPCC, *HIP_FLAGS, "-shared", *objs, "-o", tmp], cwd=PKG)
+    os.replace(tmp, out)
 
 
 def build_variant(name: str, defines: dict) -> str:
@@ -58,7 +71,7 @@ def build_variant(name: str, defines: dict) -> str:
     os.makedirs(vdir, exist_ok=True)
     out = os.path.join(vdir, f"librl_{name}.so")
     flags = [f"-D{k}={v}" for k, v in defines.items()]
-    _run([HIPCC, *HIP_FLAGS, *flags, "-shared", *KERNEL_SRCS, "-o", out], cwd=PKG)
+    _compile_link(KERNEL_SRCS, flags, out, os.path.join(vdir, "obj_" + name))
     return out
 
 

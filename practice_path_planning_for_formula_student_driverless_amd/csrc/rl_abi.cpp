@@ -406,7 +406,12 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
                 HIPCHK(hipMemsetAsync(mb.lap, 0, sizeof(double) * p->B, st));
                 HIPCHK(hipMemsetAsync(mb.sweeps, 0, sizeof(int32_t) * p->B * (p->max_outer + 1), st));
             }
-            if (p->N == 0) continue;
+            if (p->N == 0) {
+                // no kernel: record the mode's event anyway, so rl_plan_kernel_ms(1 + m)
+                // reports the (empty) interval instead of failing on an unrecorded event
+                HIPCHK(hipEventRecord(p->ev[1 + m], st));
+                continue;
+            }
         }
         (void)BN;
         rl::KParams kp;

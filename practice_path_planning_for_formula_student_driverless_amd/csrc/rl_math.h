@@ -1,7 +1,8 @@
 // rl_math.h — host+device fp64 helpers that reproduce the reference's libm calls
 // (glibc 2.35, x86-64, no FMA ifunc for hypot) using only correctly rounded
 // operations (+,-,*,/,sqrt,fma), so the gfx950 results equal the CPU's.
-// Verified against glibc on the CPU by tests/test_math_cpu.py.
+// Pinned to the host glibc by tests/test_math_cpu.py (known-answer tests, >=10^6
+// samples each: hypot bit for bit, pow15 = the correctly rounded x^1.5).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -45,7 +46,9 @@ __host__ __device__ inline double hypot_kernel(double ax, double ay) {
 }
 
 __host__ __device__ inline double hypot_ref(double x, double y) {
-    const double SCALE = 0x1p-600, LARGE_VAL = 0x1p+511, TINY_VAL = 0x1p-511, EPS = 0x1p-54;
+    // glibc's constants; TINY_VAL is 2^-459 (measured: glibc takes the scaled path for
+    // every ay < 2^-459, tests/test_math_cpu.py), which keeps the correction terms normal
+    const double SCALE = 0x1p-600, LARGE_VAL = 0x1p+511, TINY_VAL = 0x1p-459, EPS = 0x1p-54;
     if (!isfinite(x) || !isfinite(y)) {
         if (isinf(x) || isinf(y)) return INFINITY;
         return x + y;

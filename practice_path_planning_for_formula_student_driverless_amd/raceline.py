@@ -94,6 +94,17 @@ class MinTimeResult(MinCurvResult):
 
 
 # ------------------------------------------------------------------ batch API
+def _check_batch(B: int, ncfg: int, seeds) -> None:
+    """The C side reads exactly B seeds and B (or 1) cfgs (rl_abi.h): a shorter array
+    would be read past its end, so a mismatch is an error here."""
+    if B < 0:
+        raise ValueError(f"B must be >= 0, got {B}")
+    if ncfg not in (1, B):
+        raise ValueError(f"cfgs: need 1 or B={B} entries, got {ncfg}")
+    if seeds is not None and len(seeds) != B:
+        raise ValueError(f"seeds: need exactly B={B} entries, got {len(seeds)}")
+
+
 def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
                    mincurv: bool = True, mintime: bool = True):
     """Optimise B instances (seed b / cfg b) of one problem on the GPU.
@@ -104,6 +115,7 @@ def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
     cfg_arr, ncfg = abi.cfg_array(cfgs)
     if B is None:
         B = ncfg if ncfg > 1 else (len(seeds) if seeds is not None else 1)
+    _check_batch(B, ncfg, seeds)
     mo = int(cfg_arr[0].max_outer_iters)
     seeds_a = abi.seed_array(seeds)
     out_mc = Outputs.alloc(B, prob.N, mo, False) if mincurv else None
@@ -125,6 +137,7 @@ class Plan:
         cfg_arr, ncfg = abi.cfg_array(cfgs)
         if B is None:
             B = ncfg if ncfg > 1 else (len(seeds) if seeds is not None else 1)
+        _check_batch(B, ncfg, seeds)
         self.B, self.N, self.modes = B, prob.N, modes
         self.max_outer = int(cfg_arr[0].max_outer_iters)
         self._keep = (prob, cfg_arr)

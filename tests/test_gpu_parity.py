@@ -5,6 +5,8 @@ Integer outputs (evals/accepts per outer, v-pass sweeps) must match the oracle.
 """
 import os
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -489,13 +491,20 @@ def test_batch_csv_writer_matches_per_instance(tmp_path):
         assert open(bases[b] + "_raceline_with_geom.csv", "rb").read() == open(ref_base + "_raceline_with_geom.csv", "rb").read()
 
 
-
+def test_errors_fail_loudly():
+    """Bad batch shapes and oversized N are errors at both layers, never a silent run."""
     _lib_or_skip()
     case = O.load_case("track_training_map")
     prob = O.case_problem(case)
     cfg = O.case_cfg(case)
-    with pytest.raises(raceline.RacelineError):
-        raceline.optimize_batch(prob, [cfg, cfg, cfg], None, 2)          # n_cfg not 1 or B
+    with pytest.raises(ValueError):
+        raceline.optimize_batch(prob, [cfg, cfg, cfg], None, 2)          # n_cfg not 1 or B (host check)
+    with pytest.raises(ValueError):
+        raceline.optimize_batch(prob, cfg, seeds=[0, 1], B=8)            # seeds shorter than B
+    cfg_arr, _ = abi.cfg_array([cfg, cfg, cfg])
+    p = prob.as_c()
+    rc = abi.load_library().rl_optimize(C.byref(p), cfg_arr, 3, None, 2, None, None)   # the C side's own check
+    assert rc == abi.RL_EINVAL
     big = abi.Problem(center=np.zeros(((1 << 20) + 1, 2)), L=100.0, inner_seg=prob.inner_seg, outer_seg=prob.outer_seg)
     with pytest.raises(raceline.RacelineError) as ei:
         raceline.optimize_batch(big, cfg, None, 1)
