@@ -39,12 +39,6 @@ namespace rl {
 #ifndef RL_CK
 #define RL_CK 2
 #endif
-#ifndef RL_MFMA_RED
-#define RL_MFMA_RED 0    // 1: evaluation sums on the fp64 matrix core (A/B: slower)
-#endif
-#ifndef RL_SPEC_GRAD
-#define RL_SPEC_GRAD 0   // 1: interior of the next gradient ahead of the reduction (A/B: slower)
-#endif
 constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per ring pass)
 #ifndef RL_MD_TIGHT
 #define RL_MD_TIGHT 0    // fallback search: nearest-midpoint radius pass (rl_corridor.h ring_mindist; A/B: +0.8% C2 here, -21% C5 in the streaming kernel)
@@ -116,17 +110,22 @@ __device__ __forceinline__ void wave_sum2(double& x, double& y) {
     x = readlane(x, 63);
     y = readlane(y, 63);
 }
-// wave-uniform sum of x on the fp64 matrix core: with B = ones, v_mfma_f64_16x16x4
-// gives each lane the four row sums S_{4g..4g+3} of its 16-lane group g (S_i = Σ_k
-// x_{i+16k}); their sum T_g fed through a second MFMA leaves T_0+T_1+T_2+T_3 in every
-// lane.  Two MFMAs and three VALU adds instead of ~20 VALU (DPP movs, adds, readlanes).
-typedef double rl_v4d __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ double wave_sum_mfma(double x) {
-    const rl_v4d z = {0.0, 0.0, 0.0, 0.0};
-    const rl_v4d d = __builtin_amdgcn_mfma_f64_16x16x4f64(x, 1.0, z, 0, 0, 0);
-    const double t = (d[0] + d[1]) + (d[2] + d[3]);
-    const rl_v4d e = __builtin_amdgcn_mfma_f64_16x16x4f64(t, 1.0, z, 0, 0, 0);
-    return e[0];
+// IEEE maxNum / minNum on the fp64 VALU (one instruction each).  They equal the
+// reference's std::max(lo, x) / std::min(hi, x) select forms for every x unless a
+// bound is a zero: v_max_f64(-0, +0) = +0 where std::max(-0, +0) = -0, and
+// v_min_f64(+0, -0) = -0 where std::min(+0, -0) = +0.  The projection uses them only
+// in waves whose bounds hold no such zero (PGD loop, `zb`).  Inline asm: the operands
+// need no canonicalisation (a NaN trial value would be a quiet NaN, and maxNum then
+// returns the bound, as the select form does).
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 // lane l <- lane l-1 (wave_shr:1); lane 0 keeps `edge` (bound_ctrl off: no write)
 __device__ __forceinline__ double dpp_from_left_or(double x, double edge) {
@@ -172,17 +171,24 @@ __device__ __forceinline__ void put(double (&a)[K], int idx, double v) {
 template <int K, int T>
 struct alignas(16) Smem {
     static constexpr int NW = T / 64;
+    // The small tables come first: their (mostly wave-uniform) addresses then fit the
+    // 16-bit offset field of ds_read/ds_write, so one base register serves them all.
+    //
+    // Edge tables of the neighbour exchange, one row per exchange slot.  Every lane
+    // stores (branch-free): the lane that publishes into its row's tail, every other lane
+    // into its own entry of the row's head (a sink nobody reads).  One address register
+    // per table serves all four slots (the slot is an immediate offset).
+    static constexpr int RF = 64 + NW;
+    double pubF[4][RF];          // [s][64 + w]: first value of lane 0 of wave w
+    double pubL[4][RF];          // [s][64 + w]: last value of lane 63 of wave w
+    double pubW[4][65];          // [s][64]: last valid value of the last active thread (closed wrap)
+    double red[3][NW];           // per-wave partial sums of an evaluation
+    double red2[2][NW];          // other block reductions
+    double bc[4];                // broadcast scalars
     union {
         double2 coef[2][K][T];   // [0]: (A1,A2)  [1]: (N0,W)   (precompute_lin_geom_generic)
         double vin[2][T];        // v-pass relaxation: published outgoing values
     } u;
-    double eF[4][NW];            // per exchange slot: lane-0 first value of each wave
-    double eL[4][NW];            //                    lane-63 last value of each wave
-    double wL[4];                // last valid value of the last active thread (closed wrap)
-    double sink[64];             // target of the lanes that publish nothing (branch-free stores)
-    double red[3][NW];           // per-wave partial sums of an evaluation
-    double red2[2][NW];          // other block reductions
-    double bc[4];                // broadcast scalars
 };
 
 // --------------------------------------------------------------- the kernel
@@ -262,7 +268,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const int base = tid * K;
     const int Ta = (N + K - 1) / K;
     const bool active = tid < Ta;
-    const int cnt = min(K, max(0, N - base));           // samples of this thread
+    // samples of this thread (without a partial chunk: K or 0, one lane mask for every k)
+    const int cnt = RAGGED ? min(K, max(0, N - base)) : (tid < Ta ? K : 0);
     const int cntL = N - (Ta - 1) * K;                  // samples of the last active thread
     // wave-uniform: does this wave hold the (only) partial chunk?  Every other
     // lane is either full (cnt == K) or inactive, and inactive lanes carry exact
@@ -285,6 +292,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const double lam2 = 2.0 * lam;                       // ref:673 2.0*lambda_smooth*gsm
     const double lam_act = active ? lam : 0.0;           // inactive lanes' Σa1² drops out of J
     const bool is_last = tid == Ta - 1;
+    const bool wrap_lane = tail_wave && is_last;         // the closed wrap's right neighbour is sample 0
     // PGD constants in registers (the cfg lives in global memory the kernel also writes)
     const double step_init = C.step_init, step_min = C.step_min, armijo_c = C.armijo_c;
     const int max_inner = C.max_inner_iters;
@@ -299,16 +307,19 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 
     // ---- neighbour exchange (DPP in-wave, LDS across waves and for the wrap) ----
     // before a barrier: the wave's edge values (and the wrap value) go to LDS
+    double* const aF = &sm.pubF[0][(lane == 0) ? 64 + wid : lane];
+    double* const aL = &sm.pubL[0][(lane == 63) ? 64 + wid : lane];
+    double* const aW = &sm.pubW[0][(tid == Ta - 1) ? 64 : lane];
     auto xpub = [&](int slot, const double (&a)[K]) RL_AI {
         if constexpr (NW == 1) return;       // one wave: xget reads the edges with readlane
         const double first = a[0], last = a[K - 1];
-        *((lane == 0) ? &sm.eF[slot][wid] : &sm.sink[lane]) = first;
-        *((lane == 63) ? &sm.eL[slot][wid] : &sm.sink[lane]) = last;
+        aF[slot * Smem<K, T>::RF] = first;
+        aL[slot * Smem<K, T>::RF] = last;
         if (!RAGGED || cntL == K) {
-            *((tid == Ta - 1) ? &sm.wL[slot] : &sm.sink[lane]) = last;
+            aW[slot * 65] = last;
         } else if (part_wave) {
             const double lv = pick(a, cntL - 1);
-            if (tid == Ta - 1) sm.wL[slot] = lv;
+            if (tid == Ta - 1) sm.pubW[slot][64] = lv;
         }
     };
     // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped).
@@ -322,17 +333,19 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             el = readlane(lastv, Ta - 1);
             ef = readlane(a[0], 0);
         } else {
-            el = (wid > 0) ? sm.eL[slot][(wid > 0) ? wid - 1 : 0] : sm.wL[slot];   // wave-uniform reads
-            ef = sm.eF[slot][(wid + 1 < NW) ? wid + 1 : 0];
+            el = (wid > 0) ? sm.pubL[slot][64 + ((wid > 0) ? wid - 1 : 0)] : sm.pubW[slot][64];   // wave-uniform reads
+            ef = sm.pubF[slot][64 + ((wid + 1 < NW) ? wid + 1 : 0)];
         }
         lv = dpp_from_left_or(a[K - 1], el);
         rv = dpp_from_right_or(a[0], ef);
         // the closed wrap for the last active thread; inactive lanes keep whatever
         // their neighbours hold (finite) -- their coefficients and bounds are zero,
         // so only their Σa1² term could leak, and lam_act removes it
-        if (CLOSED && tail_wave) {
-            const double e0 = (NW == 1) ? ef : sm.eF[slot][0];
-            if (is_last) rv = e0;
+        // (one lane-masked select: a wave-uniform branch on tail_wave would be if-converted
+        // into a second select pair)
+        if (CLOSED) {
+            const double e0 = (NW == 1) ? ef : sm.pubF[slot][64];
+            rv = wrap_lane ? e0 : rv;
         }
     };
     // the last active thread's padding slots take the right neighbour, so every
@@ -392,9 +405,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         if (!active) return;
         double px[K + 4], py[K + 4];
         loadP(px, py);
+        const int bs = opaque(base);     // per-phase addresses (nothing hoisted across the PGD loop)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int i = base + k;
+            const int i = bs + k;
             double tx, ty;
             if (N == 1) { tx = 1; ty = 0; }
             else if (CLOSED) { tx = (px[k + 3] - px[k + 1]) * 0.5; ty = (py[k + 3] - py[k + 1]) * 0.5; }
@@ -617,15 +631,17 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 
     // ---- state ------------------------------------------------------------
     double G2[K];                                   // γ² (min-time)
-    double lo[K], hi[K], al[K], gr[K], an[K];       // corridor, α, grad, α_trial
-    double gn[K];                                   // next gradient, interior samples (speculative)
+    // corridor, α and α_trial, the gradient at α; (al, gr) and (an, gn) swap roles on
+    // every accepted step (PGD loop), so nothing is copied
+    double lo[K], hi[K], al[K], gr[K], an[K], gn[K];
     double q1[K], q2[K], a1v[K];                    // gradient stencil inputs of the last evaluation
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
     // of the trial vector a: J (uniform across the workgroup) and the Armijo
     // decrease Σ grad*(a-α) (ref:733 / 1009); q1,q2,D1α and their in-wave
     // neighbours are left for eval_grad.
-    auto eval_j = [&](double (&a)[K], bool trial, double& dec) RL_AI -> double {
+    auto eval_j = [&](double (&a)[K], const double (&cur)[K], const double (&g)[K], bool trial,
+                      double& dec) RL_AI -> double {
         // J and the Armijo decrease only steer accept/stop decisions; the α iterates
         // never read them, so their accumulations use fma (their summation order
         // already differs from the reference's serial loop, ref:661-666)
@@ -634,17 +650,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             if (part_wave) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (k < cnt) pdec = __builtin_fma(gr[k], a[k] - al[k], pdec);
+                    if (k < cnt) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
             } else {
 #pragma unroll
-                for (int k = 0; k < K; ++k) pdec = __builtin_fma(gr[k], a[k] - al[k], pdec);
+                for (int k = 0; k < K; ++k) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
             }
         }
         xpub(0, a);
         if constexpr (NW > 1) __syncthreads();
-#ifdef RL_EXP_BAR      // experiment: one extra barrier per evaluation (cost probe)
-        __syncthreads();
-#endif
         double lv, rv;
         xget(0, a, lv, rv);
         fill_pad(a, rv);
@@ -681,31 +694,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         xpub(1, q1);
         xpub(2, q2);
         xpub(3, a1v);
-#if RL_SPEC_GRAD
-        // the interior of the next gradient needs no neighbour: compute it now, ahead
-        // of the reduction (used only if the step is accepted)
-        if (!part_wave) {
-#pragma unroll
-            for (int k = 1; k + 1 < K; ++k)
-                gn[k] = grad_at(k, q1[k - 1], q1[k], q1[k + 1], q2[k - 1], q2[k], q2[k + 1], a1v[k - 1], a1v[k],
-                                a1v[k + 1]);
-        }
-#endif
-#if RL_MFMA_RED
-        pJ = wave_sum_mfma(pJ);
-#else
         if (trial) wave_sum2(pJ, pdec);
         else pJ = wave_sum(pJ);
-#endif
-#ifdef RL_EXP_RED      // experiment: one extra wave reduction per evaluation (cost probe)
-        {
-            double xx = wave_sum(pJ * 0.5);
-            asm volatile("" ::"v"(xx));
-        }
-#endif
-#if RL_MFMA_RED
-        if (trial) pdec = wave_sum_mfma(pdec);
-#endif
         if constexpr (NW == 1) {             // the wave sums are the block sums
             dec = pdec;
             return pJ;
@@ -719,33 +709,19 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         return J;
     };
     // gradient of the last evaluation (ref:668-673 / 886-893)
-    auto eval_grad = [&]() RL_AI {
+    auto eval_grad = [&](double (&g)[K]) RL_AI {
         double l1, r1, l2, r2, l3, r3;
         xget(1, q1, l1, r1);
         xget(2, q2, l2, r2);
         xget(3, a1v, l3, r3);
-        auto full = [&]() RL_AI {
-            fill_pad(q1, r1);
-            fill_pad(q2, r2);
-            fill_pad(a1v, r3);
+        fill_pad(q1, r1);
+        fill_pad(q2, r2);
+        fill_pad(a1v, r3);
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                gr[k] = grad_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
-                                (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
-                                (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
-        };
-#if RL_SPEC_GRAD
-        if (part_wave) {
-            full();
-        } else {
-            gr[0] = grad_at(0, l1, q1[0], q1[1], l2, q2[0], q2[1], l3, a1v[0], a1v[1]);
-#pragma unroll
-            for (int k = 1; k + 1 < K; ++k) gr[k] = gn[k];
-            gr[K - 1] = grad_at(K - 1, q1[K - 2], q1[K - 1], r1, q2[K - 2], q2[K - 1], r2, a1v[K - 2], a1v[K - 1], r3);
-        }
-#else
-        full();
-#endif
+        for (int k = 0; k < K; ++k)
+            g[k] = grad_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
+                            (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
+                            (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
     };
 
     // ======================================================================
@@ -770,11 +746,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     RL_STAMP(0);
     for (int outer = 0;; ++outer) {
         if (outer > 0 && active) {
+            const int bu = opaque(base);
             // update (ref:743-746 / 1027-1030): alpha_last, P += n*alpha, alpha_accum
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (k < cnt) {
-                    const int i = base + k;
+                    const int i = bu + k;
                     ALAST[i] = al[k];
                     X[i] += NX[i] * al[k];
                     Y[i] += NY[i] * al[k];
@@ -793,13 +770,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             __syncthreads();
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
             corridor(guard, lo, hi);
-#ifdef RL_EXP_CORR2    // experiment: the corridor twice (cost probe; same results)
-            corridor(guard, lo, hi);
-#endif
             if (outer == 0 && seed != 0) {                      // ref:720 + seed
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    double s0 = seed_value(seed, base + k, RL_SEED_SIGMA);
+                    // (opaque: keeps the seed values from being hoisted out of the outer
+                    // loop, where they would hold 2K VGPRs for the whole kernel)
+                    double s0 = seed_value(seed, opaque(base) + k, RL_SEED_SIGMA);
                     al[k] = (k < cnt) ? smin(hi[k], smax(lo[k], s0)) : 0.0;
                 }
             }
@@ -825,7 +801,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             if (outer == MO && active) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (k < cnt) { p.heading[off + base + k] = hd[k]; p.kappa[off + base + k] = ka[k]; }
+                    if (k < cnt) { p.heading[off + opaque(base) + k] = hd[k]; p.kappa[off + opaque(base) + k] = ka[k]; }
             }
         }
         if (MT) {
@@ -925,51 +901,71 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
         RL_STAMP(3);
         // PGD + Armijo (ref:723-742 / 996-1026)
+        // zb: this wave's bounds hold a zero of the sign that makes maxNum/minNum differ
+        // from the reference's select forms (lo = -0, or hi = +0 on a valid sample;
+        // padding and inactive lanes hold lo = hi = +0, where both forms agree).
+        // Wave-uniform, fixed for the outer iteration.
+        bool zb_lane = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            zb_lane |= (__double_as_longlong(lo[k]) == (long long)0x8000000000000000ull) ||
+                       (hi[k] == 0.0 && k < cnt);
+        const bool zb = __builtin_amdgcn_ballot_w64(zb_lane) != 0;
         double step = step_init;
+        // trial vector std::min(hi, std::max(lo, cur - step*grad)) (ref:731)
+        auto project = [&](const double (&cur)[K], const double (&g)[K], double (&nxt)[K]) RL_AI {
+            double ai[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) ai[k] = cur[k] - step * g[k];
+            if (!zb) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) nxt[k] = vmin_f64(hi[k], vmax_f64(lo[k], ai[k]));
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) nxt[k] = smin(hi[k], smax(lo[k], ai[k]));   // the select forms
+            }
+        };
         double dec;
-        double J = eval_j(al, false, dec);
-        eval_grad();
-        int evals = 1, accepts = 0;
+        double J = eval_j(al, al, gr, false, dec);
+        eval_grad(gr);
+        int evals = 1, accepts = 0, it = 0;
         double J_prev = J;
-        for (int it = 0; it < max_inner; ++it) {
-            bool accepted = false;
+        // One inner iteration (ref:726-742) from (cur, gc): trials in nxt, the gradient of
+        // an accepted trial into gx.  Returns 2: accepted, go on (nxt is current); 1: stop
+        // with nxt current; 0: stop with cur current.  The loop below alternates the
+        // roles of (al, gr) and (an, gn), so an accepted step copies nothing.
+        auto inner = [&](const double (&cur)[K], const double (&gc)[K], double (&nxt)[K], double (&gx)[K]) RL_AI -> int {
+            if (it >= max_inner) return 0;
+            ++it;
             int bt = 0;
-            while (bt < 20) {
-                // std::min(hi, std::max(lo, ai)) (ref:731) as selects: v_min/v_max_f64
-                // would return the other zero when lo = -0 / hi = +0 meet a zero, and
-                // alpha_last is printed with its sign (ref:1372).  In phases, with each
-                // compare in its own lane mask, so no select waits on the compare just
-                // before it (VALU-written mask hazard).
-                double ai[K], mm[K];
-                uint64_t cm[K];
-#pragma unroll
-                for (int k = 0; k < K; ++k) ai[k] = al[k] - step * gr[k];
-#pragma unroll
-                for (int k = 0; k < K; ++k) cm[k] = __builtin_amdgcn_ballot_w64(lo[k] < ai[k]);
-#pragma unroll
-                for (int k = 0; k < K; ++k) mm[k] = __builtin_amdgcn_inverse_ballot_w64(cm[k]) ? ai[k] : lo[k];
-#pragma unroll
-                for (int k = 0; k < K; ++k) cm[k] = __builtin_amdgcn_ballot_w64(mm[k] < hi[k]);
-#pragma unroll
-                for (int k = 0; k < K; ++k) an[k] = __builtin_amdgcn_inverse_ballot_w64(cm[k]) ? mm[k] : hi[k];
-                double Jn = eval_j(an, true, dec);
+            for (;;) {
+                project(cur, gc, nxt);
+                double Jn = eval_j(nxt, cur, gc, true, dec);
                 ++evals;
                 if (Jn <= J + armijo_c * dec) {
-#pragma unroll
-                    for (int k = 0; k < K; ++k) al[k] = an[k];
-                    eval_grad();
+                    eval_grad(gx);
                     J = Jn;
-                    accepted = true;
                     ++accepts;
                     break;
                 }
                 step *= 0.5;
                 bt++;
-                if (step < step_min) break;
+                if (step < step_min || bt >= 20) return 0;
             }
-            if (!accepted) break;
-            if (fabs(J_prev - J) < 1e-10) break;
+            if (fabs(J_prev - J) < 1e-10) return 1;
             J_prev = J;
+            return 2;
+        };
+        bool in_an = false;
+        for (;;) {
+            int r = inner(al, gr, an, gn);
+            if (r != 2) { in_an = (r == 1); break; }
+            r = inner(an, gn, al, gr);
+            if (r != 2) { in_an = (r == 0); break; }
+        }
+        if (in_an) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) al[k] = an[k];
         }
         if (tid == 0) {
             if (p.evals) p.evals[(size_t)b * MO + outer] = evals;
@@ -1042,6 +1038,9 @@ static int cu_count() {
 
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
+#ifdef RL_ANALYZE_ONE   // static analysis builds (scripts/regs.sh -one): the C2/C3 shape only
+    return mintime ? launch_t<8, 256, true, true>(p, st) : launch_t<8, 256, true, false>(p, st);
+#else
     if (p.N <= 4 * 64) return launch_kt<4, 64>(p, mintime, st);
     if (p.N <= 8 * 64) return launch_kt<8, 64>(p, mintime, st);      // one wave (single-wave paths)
     if (p.N <= 8 * 128) return launch_kt<8, 128>(p, mintime, st);
@@ -1056,6 +1055,7 @@ hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
         return launch_ktm<RL_MIDMT_K, RL_MIDMT_T, true>(p, st);
     }
     return launch_kt<8, 512>(p, mintime, st);
+#endif
 }
 
 }  // namespace rl

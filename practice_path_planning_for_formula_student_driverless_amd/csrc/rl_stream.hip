@@ -377,9 +377,6 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             }
 #else
             for (int i = tid; i < N; i += TS) {
-#ifdef RL_EXP_CORR2
-                corridor_at(i, guard);
-#endif
                 corridor_at(i, guard);
                 if (outer == 0 && seed != 0)
                     al_p[i] = smin(HI[i], smax(LO[i], seed_value(seed, i, RL_SEED_SIGMA)));

@@ -10,9 +10,6 @@ VARIANTS = {
     "k4t512w4": {"RL_MID_K": 4, "RL_MID_T": 512, "RL_MID_W": 4},
     "ck4": {"RL_CK": 4},
     "mt_k8t256": {"RL_MIDMT_K": 8, "RL_MIDMT_T": 256},
-    "exp_corr2": {"RL_EXP_CORR2": 1},
-    "exp_bar": {"RL_EXP_BAR": 1},
-    "exp_red": {"RL_EXP_RED": 1},
     "old_w": {"RL_SMALLMT_W": 4, "RL_SMALL_W": 4, "RL_S8MT_W": 2},   # before the per-mode occupancy A/B
     "smc_w4": {"RL_SMALL_W": 4},
     "smc_w3": {"RL_SMALL_W": 3},
