@@ -127,6 +127,33 @@ __device__ __forceinline__ double vmin_f64(double a, double b) {
     asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// x + (the same register of the lane 16 (permlane16) / 32 (permlane32) rows away): the
+// swap exchanges the odd rows of one copy with the even rows of the other, so the two
+// copies afterwards hold (r0,r0,r2,r2) and (r1,r1,r3,r3) (resp. the half-waves), and their
+// sum is r0+r1 in rows 0-1 and r2+r3 in rows 2-3 (resp. lo+hi everywhere)
+__device__ __forceinline__ double swap16_add(double x) {
+    const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
+    return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+__device__ __forceinline__ double swap32_add(double x) {
+    const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
+    return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+// Two wave sums in one butterfly: the first step leaves x-pair sums in the even lanes
+// and y-pair sums in the odd lanes; every later step (quad_perm [2,3,0,1], row_ror 4/8,
+// the row and half-wave swaps) keeps lane parity, so one chain serves both sums.
+// Returns Σx in every even lane and Σy in every odd lane.
+__device__ __forceinline__ double wave_sum_xy(double x, double y, bool odd) {
+    const double send = odd ? x : y, keep = odd ? y : x;
+    double z = keep + dpp<0xB1>(send);    // quad_perm [1,0,3,2]: the partner lane l^1
+    z += dpp<0x4E>(z);                     // quad_perm [2,3,0,1]
+    z += dpp<0x124>(z);                    // row_ror:4
+    z += dpp<0x128>(z);                    // row_ror:8: row sums
+    z = swap16_add(z);
+    return swap32_add(z);
+}
 // lane l <- lane l-1 (wave_shr:1); lane 0 keeps `edge` (bound_ctrl off: no write)
 __device__ __forceinline__ double dpp_from_left_or(double x, double edge) {
     int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x138, 0xf, 0xf, false);
@@ -694,17 +721,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         xpub(1, q1);
         xpub(2, q2);
         xpub(3, a1v);
-        if (trial) wave_sum2(pJ, pdec);
-        else pJ = wave_sum(pJ);
+        const double z = wave_sum_xy(pJ, pdec, lane & 1);   // lane 0: Σ J terms, lane 1: Σ decrease
         if constexpr (NW == 1) {             // the wave sums are the block sums
-            dec = pdec;
-            return pJ;
+            dec = readlane(z, 1);
+            return readlane(z, 0);
         }
-        if (lane == 0) { sm.red[0][wid] = pJ; sm.red[2][wid] = pdec; }
+        if (lane < 2) sm.red[lane][wid] = z;
         __syncthreads();
-        double J = sm.red[0][0], D = sm.red[2][0];
+        double J = sm.red[0][0], D = sm.red[1][0];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) { J += sm.red[0][w]; D += sm.red[2][w]; }
+        for (int w = 1; w < NW; ++w) { J += sm.red[0][w]; D += sm.red[1][w]; }
         dec = D;
         return J;
     };
