@@ -4,24 +4,29 @@
 Workload (BASELINE.json configs[1] = SURVEY.md §8d C2): competition_map1 closed,
 N=2000 resample, B=1024 α-seeds per GPU, min-curvature optimiser, default cfg
 (14 outer iterations).  One *step* = one launch optimising the whole batch from
-inputs already resident in HBM; for N>1 the step also gathers the results
-(x, y, κ, α_last, evals) to rank 0 with RCCL over xGMI (the only collective).
-Weak scaling: every rank optimises its own 1024 seeds.
+inputs already resident in HBM; for N>1 the step also gathers per-instance
+summaries to rank 0 with RCCL over xGMI (the only collective).  Weak scaling:
+every rank optimises its own 1024 seeds.
 
 value = (instances x 14 outer iterations, all ranks) / (max over ranks of the
-timed K steps).  Also reported: tracks/s, parity of seed 0 against the
-reference's own fixture, the min-time lap-time Δ (C3 workload, N=2000,
-max_vpass_iters=20) and the single-thread CPU baseline (the C oracle, a bounded
-sample of the same workload) timed on this host.
+timed K steps).  Also reported (rank 0): C3/C4/C5, the PCIe-inclusive C2 rate,
+the drop-in B=1 latency per bundled track next to the reference's own CPU time,
+lap-time Δ statistics over instances against the CPU oracle, and the CPU
+baseline (the reference compiled from its sources, oracle/_ref, on one pinned
+core; the C restatement beside it).  The CPU work runs in a child process
+started before any GPU call (`--cpu-leg`), pinned away from the GPU host thread.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu] [--no-extras]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -34,10 +39,41 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 from practice_path_planning_for_formula_student_driverless_amd import abi, raceline  # noqa: E402
 from practice_path_planning_for_formula_student_driverless_amd import distributed as D  # noqa: E402
 
-# fp64 peak on MI355X (AMD spec: FP64 vector = FP64 dense matrix = 78.6 TFLOP/s;
-# the path runs on the fp64 VALU, there is no MFMA-shaped contraction in it).
+# MI355X fp64 vector peak (AMD spec, FMA counted as 2 flops; equal to the fp64 dense
+# matrix peak).  The path is fp64 VALU arithmetic; most of its operations are plain
+# add/mul (-ffp-contract=off keeps the reference's roundings), for which the same pipe
+# peaks at half that rate.
 FP64_PEAK_TFLOPS = 78.6
+FP64_NONFMA_TFLOPS = 39.3
 HBM_PEAK_GBS = 8000.0
+PKG = os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd")
+C4_ITEMS = 7 * 512
+C3_BATCH = 4096
+C3_SAMPLE = 128            # C3 instances whose laps the CPU oracle recomputes (strided over the batch)
+DROPIN_CASES = ["track_" + t for t in D.C4_TRACKS] + ["cmap1_n2000"]
+
+
+def source_sha() -> str:
+    """Hash of the kernel sources: a PMC summary is used only if measured on this code."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(PKG, "csrc", "*"))) + [os.path.join(REPO, "include", "rl_abi.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def read_pmc(tag: str):
+    """The committed rocprofv3 PMC summary for `tag` (profiles/pmc_traffic.json, written by
+    scripts/pmc_summary.py --commit), or None when it was measured on other kernel sources."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p)).get(tag)
+    except Exception:
+        return None
+    if not d or d.get("source_sha") != source_sha():
+        return None
+    return d
 
 
 def load_problem(name: str):
@@ -47,58 +83,223 @@ def load_problem(name: str):
     return case, O.case_problem(case), O.case_cfg(case)
 
 
-def flops_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: float = 0.0) -> float:
+def flops_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False) -> float:
     """Algorithmic fp64 flops per outer iteration, SURVEY.md §8d's per-unit figure:
-    34 (min-curv) / 36 (min-time) per sample per evaluation, plus the corridor's
-    2·(Ei+Eo) ray tests per sample at 12 flops + 1 reciprocal each.  (The kernel
-    skips most ray tests exactly — rl_corridor.h — so it executes fewer; the
-    executed count from the PMC counters is reported beside it.)"""
+    34 (min-curv) / 36 (min-time) per sample per evaluation, plus the reference's
+    2·(Ei+Eo) ray tests per sample at 12 flops + 1 reciprocal each (the kernel culls
+    most ray tests exactly, so it executes fewer: see executed_fp64_TFLOPs_pmc)."""
     per_eval = 36.0 if mintime else 34.0
     return N * (per_eval * E_k + 2 * Eseg * 13)
 
 
-def bytes_per_outer(N: int, E_k: float, Eseg: int, mintime: bool = False, S: float = 0.0) -> float:
-    """SURVEY.md §8d streaming model (8-B words, each array once per pass)."""
-    if mintime:
-        return N * (88 * E_k + 224 + 24 + 48 * S + 32) + 32 * Eseg
+def bytes_per_outer(N: int, E_k: float, Eseg: int) -> float:
+    """SURVEY.md §8d streaming model (8-B words, each array once per evaluation pass)."""
     return N * (80 * E_k + 224) + 32 * Eseg
 
 
-def read_pmc(tag: str, key: str = "hbm_bytes_per_launch"):
-    """Per-launch figure (HBM bytes, executed fp64 flops) from the committed rocprofv3
-    PMC summary profiles/pmc_traffic.json (scripts/pmc.sh + pmc_summary.py), or None."""
-    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
+# ============================================================ CPU leg (child process)
+def _cpu_info() -> dict:
+    model = ""
     try:
-        with open(p) as f:
-            d = json.load(f)
-        return d.get(tag, {}).get(key)
-    except Exception:
-        return None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
 
-def cpu_baseline(prob, cfg, budget_s: float = 12.0, max_inst: int = 64):
-    """Single-thread C oracle on a bounded sample of the same workload (seeds 0..)."""
+class _RefHarness:
+    """oracle/_ref/libref_harness.so: the reference's own main.cpp compiled from its
+    sources (oracle/Makefile `ref`, built in the build container; absent -> None)."""
+
+    def __init__(self):
+        import ctypes as C
+
+        import oracle_lib as O
+
+        self.C = C
+        self.lib = C.CDLL(O.REF_SO)
+        d = C.POINTER(C.c_double)
+        common = [d, C.c_int, C.c_double, C.c_int, d, C.c_int, d, C.c_int, C.c_double] + [d] * 6
+        self.lib.ref_min_curv.argtypes = common
+        self.lib.ref_min_time.argtypes = common + [d, d, d]
+        self.lib.ref_cfg_apply.argtypes = [C.POINTER(abi.RlCfg)]
+        self.lib.ref_cfg_reset()
+
+    def run(self, prob, cfg, mintime: bool) -> float:
+        """One compute_min_curvature_raceline / compute_min_time_raceline call (ref:683 /
+        905) on the problem; returns the lap (min-time) or 0."""
+        C = self.C
+        self.lib.ref_cfg_reset()
+        self.lib.ref_cfg_apply(C.byref(cfg))
+        N = prob.N
+        outs = [np.zeros(max(N, 1)) for _ in range(8)]
+        lap = np.zeros(1)
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))   # noqa: E731
+        args = [dp(np.ascontiguousarray(prob.center)), N, prob.L, 1 if prob.closed else 0,
+                dp(np.ascontiguousarray(prob.inner_seg)), prob.inner_seg.shape[0],
+                dp(np.ascontiguousarray(prob.outer_seg)), prob.outer_seg.shape[0], prob.veh_width]
+        if mintime:
+            rc = self.lib.ref_min_time(*args, *[dp(o) for o in outs], dp(lap))
+        else:
+            rc = self.lib.ref_min_curv(*args, *[dp(o) for o in outs[:6]])
+        if rc != 0:
+            raise RuntimeError("reference harness failed")
+        return float(lap[0])
+
+
+def _ref_harness():
     import oracle_lib as O
 
-    seeds = np.arange(max_inst, dtype=np.uint64)
-    done = 0
-    t0 = time.perf_counter()
-    while done < max_inst and time.perf_counter() - t0 < budget_s:
-        O.run_oracle(prob, cfg, seeds=seeds, B=max_inst, modes=(True, False), b_range=(done, done + 1))
-        done += 1
+    return _RefHarness() if os.path.exists(O.REF_SO) else None
+
+
+def _lap_worker(job):
+    """Pool worker (CPU only): min-time laps of (case, cfg dict, seed) jobs with the C oracle."""
+    import oracle_lib as O
+
+    out = []
+    cache = {}
+    for name, cfgd, seed in job:
+        if name not in cache:
+            cache[name] = O.case_problem(O.load_case(name))
+        c = abi.RlCfg.from_dict(cfgd)
+        _, mt = O.run_oracle(cache[name], [c], seeds=[seed], B=1, modes=(False, True))
+        out.append(float(mt.lap[0]))
+    return out
+
+
+def cpu_leg(budget_s: float) -> dict:
+    """Everything the bench needs from the CPU, computed without touching the GPU:
+    the baseline on one pinned core, the reference's per-track drop-in times, and the
+    oracle laps the GPU laps are compared with (process pool on the other cores)."""
+    import multiprocessing as mp
+
+    import oracle_lib as O
+
+    cores = sorted(os.sched_getaffinity(0))
+    os.sched_setaffinity(0, {cores[0]})
+    info = _cpu_info()
+    res = {"cpu": info}
+    case, prob, cfg = load_problem("cmap1_n2000")
+    MO = int(cfg.max_outer_iters)
+    ref = _ref_harness()
+    # ---- baseline: C2 min-curvature at N=2000 on one core
+    if ref is not None:
+        n, t0 = 0, time.perf_counter()
+        while n == 0 or time.perf_counter() - t0 < budget_s:
+            ref.run(prob, cfg, False)
+            n += 1
+        dt = time.perf_counter() - t0
+        res["reference"] = {"value": n * MO / dt, "unit": "PGD outer-iters/s", "cores": 1, "kind": "reference",
+                            "sample": f"{n} calls of the reference's compute_min_curvature_raceline (main.cpp:683-764, "
+                                      f"oracle/_ref built from /root/reference/src/main.cpp) on C2's problem "
+                                      f"(competition_map1, N={prob.N}, alpha=0 start), {MO} outer each, {dt:.1f} s, "
+                                      f"one thread pinned to core {cores[0]}"}
+    n, t0 = 0, time.perf_counter()
+    seeds = np.arange(256, dtype=np.uint64)
+    while n < len(seeds) and (n == 0 or time.perf_counter() - t0 < budget_s / 2):
+        O.run_oracle(prob, cfg, seeds=seeds, B=len(seeds), modes=(True, False), b_range=(n, n + 1))
+        n += 1
     dt = time.perf_counter() - t0
-    outers = done * int(cfg.max_outer_iters)
-    return {"value": outers / dt, "unit": "PGD outer-iters/s", "cores": 1, "kind": "port",
-            "sample": f"{done} instances (seeds 0..{done - 1}) of C2 min-curv, N={prob.N}, 14 outer each, "
-                      f"{dt:.1f} s, one thread"}
+    res["port"] = {"value": n * MO / dt, "unit": "PGD outer-iters/s", "cores": 1, "kind": "port",
+                   "sample": f"{n} C2 instances (seeds 0..{n - 1}) through the C restatement of main.cpp:683-1052 "
+                             f"(oracle/raceline_oracle.c), {dt:.1f} s, one thread pinned to core {cores[0]}"}
+    # ---- the drop-in use (one instance per call, ref:1347 / 1397): the reference per track
+    if ref is not None:
+        per = {}
+        for name in DROPIN_CASES:
+            _, p, c = load_problem(name)
+            ts = []
+            for mintime in (False, True):
+                t0 = time.perf_counter()
+                ref.run(p, c, mintime)
+                ts.append(1e3 * (time.perf_counter() - t0))
+            per[name] = {"N": p.N, "mincurv_ms": round(ts[0], 2), "mintime_ms": round(ts[1], 2)}
+        res["reference_per_track"] = per
+    # ---- oracle laps for the lap-Δ statistics (C3 sample, the whole C4 grid)
+    c3case, _, cfg3 = load_problem("cmap1_n2000_vp20")
+    c3_seeds = list(range(0, C3_BATCH, C3_BATCH // C3_SAMPLE))
+    jobs = [("cmap1_n2000_vp20", cfg3.to_dict(), s) for s in c3_seeds]
+    base = O.case_cfg(O.load_case("track_training_map"))
+    cfgs = D.c4_cfgs(base)
+    c4_jobs = [("track_" + D.C4_TRACKS[t], cfgs[k].to_dict(), 0) for t, k in D.c4_items()]
+    workers = max(1, min(15, len(cores) - 2))
+    pool_cores = set(cores[2:2 + workers]) or {cores[-1]}
+    os.sched_setaffinity(0, pool_cores)
+    t0 = time.perf_counter()
+    chunks = lambda js, n: [js[i::n] for i in range(n)]   # noqa: E731
+    with mp.get_context("spawn").Pool(workers) as pool:
+        r3 = pool.map(_lap_worker, chunks(jobs, workers))
+        r4 = pool.map(_lap_worker, chunks(c4_jobs, workers))
+    unchunk = lambda rs, n, total: [rs[i % n][i // n] for i in range(total)]   # noqa: E731
+    res["c3_oracle_laps"] = {"seeds": c3_seeds, "laps": unchunk(r3, workers, len(jobs))}
+    res["c4_oracle_laps"] = unchunk(r4, workers, len(c4_jobs))
+    res["oracle_pool"] = {"workers": workers, "seconds": round(time.perf_counter() - t0, 1)}
+    return res
+
+
+def start_cpu_leg(budget_s: float):
+    """The CPU leg as a child process (before the parent touches the GPU).  The parent
+    then keeps to the cores the child does not use first."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-leg", "--cpu-budget", str(budget_s)]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    cores = sorted(os.sched_getaffinity(0))
+    if len(cores) > 1:
+        os.sched_setaffinity(0, {cores[1]})
+    return proc
+
+
+def finish_cpu_leg(proc):
+    out, err = proc.communicate(timeout=900)
+    if proc.returncode != 0:
+        sys.stderr.write(err[-4000:])
+        return None
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def lap_delta(gpu, oracle) -> dict:
+    d = np.abs(np.asarray(gpu, dtype=np.float64) - np.asarray(oracle, dtype=np.float64))
+    rel = d / np.abs(np.asarray(oracle, dtype=np.float64))
+    return {"n": int(d.size), "max_abs_s": float(d.max()), "mean_abs_s": float(d.mean()),
+            "max_rel": float(rel.max()), "tolerance_rel": 1e-4}
+
+
+# ============================================================== GPU legs
+def run_c3(rank, local, stream, reps: int = 3):
+    """C3: N=2000, max_vpass_iters=20, 4096 seeds per GPU, min-curv + min-time."""
+    c3, p3, cfg3 = load_problem("cmap1_n2000_vp20")
+    MO = int(cfg3.max_outer_iters)
+    pl3 = raceline.Plan(p3, cfg3, seeds=np.arange(rank * C3_BATCH, (rank + 1) * C3_BATCH, dtype=np.uint64),
+                        B=C3_BATCH, modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, device=local)
+    pl3.run(stream.cuda_stream)
+    stream.synchronize()
+    walls, kmc, kmt = [], [], []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        pl3.run(stream.cuda_stream)          # inputs resident; results stay in HBM (fetched below)
+        stream.synchronize()
+        walls.append(time.perf_counter() - t1)
+        kmc.append(pl3.kernel_ms(1))
+        kmt.append(pl3.kernel_ms(2))
+    mc3, mt3 = pl3.fetch()
+    pl3.close()
+    t3 = float(np.mean(walls))
+    return {"instances": C3_BATCH, "reps": reps, "wall_ms_mean": round(t3 * 1e3, 2),
+            "wall_ms_min": round(min(walls) * 1e3, 2), "outer_iters_per_s": round(2 * C3_BATCH * MO / t3, 1),
+            "kernel_ms_mincurv": round(float(np.mean(kmc)), 3), "kernel_ms_mintime": round(float(np.mean(kmt)), 3),
+            "lap_seed0_s": float(mt3.lap[0]), "lap_ref_s": float(c3["mt_lap"]),
+            "lap_seed0_delta_vs_reference_s": float(abs(mt3.lap[0] - float(c3["mt_lap"]))),
+            "lap_mean_over_seeds_s": float(np.mean(mt3.lap)),
+            "vpass_sweeps_mean": float(np.mean(mt3.vpass_sweeps))}, mt3.lap
 
 
 def run_c4(world, rank, local, dev, dist):
     """C4: 7 bundled tracks x 512 (mu, P_max_W, lambda_smooth) points, min-curv + min-time.
     Items are sharded track-major over ranks; one plan per track, all plans on
-    concurrent HIP streams; laps gathered to rank 0."""
+    concurrent HIP streams; laps gathered to rank 0 in item order."""
     import torch
 
     groups = D.c4_shard(world, rank)
@@ -128,28 +329,19 @@ def run_c4(world, rank, local, dev, dist):
     dt = (time.perf_counter() - t0) / reps
     n_inst = sum(len(ks) for _, ks, _ in meta)
     laps = np.concatenate([pl.fetch()[1].lap for pl in plans])
-    # parity spot check (outside timing): first sweep point of this rank's first track vs the oracle
-    import oracle_lib as O
-    t, ks, prob = meta[0]
-    _, omt = O.run_oracle(prob, [cfgs[ks[0]]], B=1, modes=(False, True))
-    lap_delta = float(abs(laps[0] - omt.lap[0]))
-    stats = torch.tensor([dt, float(n_inst), lap_delta], dtype=torch.float64, device=dev)
-    if dist is not None:
-        per = D.pad_to(3584, world)
-        lt = torch.zeros(per, dtype=torch.float64, device=dev)
-        lt[:len(laps)] = torch.from_numpy(laps)
-        got = D.gather_to_root({"laps": lt, "stats": stats}, world, rank)
-        if rank != 0:
-            return None
-        all_stats = torch.stack(got["stats"]).cpu().numpy()
-        dt, n_inst, lap_delta = float(all_stats[:, 0].max()), int(all_stats[:, 1].sum()), float(all_stats[:, 2].max())
-        laps = np.concatenate([g.cpu().numpy()[: int(s[1])] for g, s in zip(got["laps"], all_stats)])
     for pl in plans:
         pl.close()
+    if dist is not None:
+        stats = torch.tensor([[dt, float(n_inst)]], dtype=torch.float64, device=dev)
+        allst = D.gather_rows(stats, world, rank)
+        laps = D.gather_ragged(laps, world, rank, C4_ITEMS, device=dev)
+        if rank != 0:
+            return None, None
+        allst = allst.cpu().numpy()
+        dt, n_inst = float(allst[:, 0].max()), int(allst[:, 1].sum())
     return {"instances": int(n_inst), "modes": "min-curv + min-time", "ms": round(dt * 1e3, 3),
             "tracks_per_s": round(n_inst / dt, 1), "outer_iters_per_s": round(2 * 14 * n_inst / dt, 1),
-            "lap_min_s": float(laps.min()), "lap_max_s": float(laps.max()),
-            "lap_delta_vs_oracle_s": lap_delta}
+            "lap_min_s": float(laps.min()), "lap_max_s": float(laps.max())}, laps
 
 
 def run_c5(world, rank, local, dev, dist):
@@ -166,34 +358,70 @@ def run_c5(world, rank, local, dev, dist):
     if dist is not None:
         dist.barrier()
     ms = []
-    for _ in range(2):
+    for _ in range(3):
         plan.run()
         ms.append(plan.kernel_ms(1))
     k_ms = float(np.mean(ms))
     E_k = float(mc.evals.mean())
     Eseg = prob.inner_seg.shape[0] + prob.outer_seg.shape[0]
-    by = B * 14 * bytes_per_outer(prob.N, E_k, Eseg)
+    model = B * 14 * bytes_per_outer(prob.N, E_k, Eseg)
     rel = float(np.max(np.abs(mc.x[0] - case["mc_x"])) / np.max(np.abs(case["mc_x"]))) if s == 0 else 0.0
     plan.close()
-    st = torch.tensor([k_ms, rel], dtype=torch.float64, device=dev)
     if dist is not None:
-        got = D.gather_to_root({"st": st}, world, rank)
+        st = torch.tensor([[k_ms, rel]], dtype=torch.float64, device=dev)
+        arr = D.gather_rows(st, world, rank)
         if rank != 0:
             return None
-        arr = torch.stack(got["st"]).cpu().numpy()
+        arr = arr.cpu().numpy()
         k_ms, rel = float(arr[:, 0].max()), float(arr[:, 1].max())
+    pmc = read_pmc("c5_mincurv")
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "rl_stream_kernel<closed,mincurv>",
+            "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+            "achieved": round(pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9, 1) if pmc else None,
+            "frac": round(pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pmc else None,
+            "basis": "measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes, "
+                     "profiles/pmc_traffic.json at these kernel sources) / kernel time",
+            "pmc_profile": pmc.get("profile") if pmc else None,
+            "model_GBps_aside": round(model / (k_ms * 1e-3) / 1e9, 1),
+            "model_note": "SURVEY §8d one-pass-per-evaluation streaming bytes; batched backtracking reads the state "
+                          "once per 4 trial steps, so this model is not a roofline for this kernel"}
     return {"instances": world * B, "N": prob.N, "kernel_ms": round(k_ms, 3),
             "outer_iters_per_s": round(world * B * 14 / (k_ms * 1e-3), 1), "evals_per_outer": E_k,
-            "roofline": {"bound": "hbm", "achieved": round(by / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(by / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": read_pmc("c5_mincurv"),
-                         "measured_hbm_GBps": (round(read_pmc("c5_mincurv") / (k_ms * 1e-3) / 1e9, 1)
-                                               if read_pmc("c5_mincurv") else None),
-                         "model": "SURVEY §8d streaming bytes N*(80*E_k+224)+32*E per outer",
-                         "note": "frac > 1 is possible: batched backtracking reads the state once per 4 trial "
-                                 "steps, below the one-pass-per-evaluation model; measured_hbm_GBps is the "
-                                 "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE rate"},
-            "seed0_vs_reference_max_rel_err": rel}
+            "roofline": roof, "seed0_vs_reference_max_rel_err": rel}
+
+
+def run_dropin(local):
+    """The reference's own use: one instance per call (pipeline::compute_raceline_and_save
+    ref:1347 and compute_mintime_and_save ref:1397), host buffers in and out (PCIe
+    included), for the 7 bundled tracks and competition_map1 at N=2000."""
+    out = {}
+    for name in DROPIN_CASES:
+        case, prob, cfg = load_problem(name)
+        raceline.optimize_batch(prob, cfg, None, 1)            # warm-up (module load, first launch)
+        t = {"mincurv": [], "mintime": []}
+        for _ in range(5):
+            for mode in ("mincurv", "mintime"):
+                t0 = time.perf_counter()
+                raceline.optimize_batch(prob, cfg, None, 1, mincurv=mode == "mincurv", mintime=mode == "mintime")
+                t[mode].append(1e3 * (time.perf_counter() - t0))
+        out[name] = {"N": prob.N, "mincurv_ms": round(float(np.median(t["mincurv"])), 3),
+                     "mintime_ms": round(float(np.median(t["mintime"])), 3)}
+    return out
+
+
+def run_c2_pcie(prob, cfg, B, MO, rank):
+    """C2 through the synchronous host-buffer entry point rl_optimize: device
+    allocation, upload, kernel, download of all result columns (PCIe included)."""
+    seeds = np.arange(rank * B, (rank + 1) * B, dtype=np.uint64)
+    raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"call_ms_median": round(t * 1e3, 2), "outer_iters_per_s": round(B * MO / t, 1),
+            "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8)}
 
 
 def run_step6(world, rank):
@@ -213,18 +441,14 @@ def run_step6(world, rank):
         rows, kms_i = raceline.compute_geom(gp, cfg, return_ms=True)
         walls.append(time.perf_counter() - t0)
         kms.append(kms_i)
-    t0 = time.perf_counter()
-    O.run_oracle_geom(gp, cfg)
-    cpu_s = time.perf_counter() - t0
     return {"rows": int(rows.shape[0]), "segments": int(gp.inner_seg.shape[0] + gp.outer_seg.shape[0]),
             "kernel_ms": round(float(np.median(kms)), 4), "wall_ms_incl_transfers": round(1e3 * float(np.median(walls)), 3),
-            "cpu_oracle_ms_1core": round(1e3 * cpu_s, 3),
             "csv_bytes_equal_reference": raceline.format_geom_csv(rows).encode() == case["_csv"]}
 
 
 def run_lapeval(world, rank, racelines):
     """batched lap evaluations (heading/kappa + v-pass, h = L/N) of the
-    C2 run's 1024 optimised racelines (rank 0's), GPU vs the CPU oracle on a sample."""
+    C2 run's 1024 optimised racelines (rank 0's), GPU, checked on a sample against the oracle."""
     import oracle_lib as O
 
     if rank != 0:
@@ -237,21 +461,18 @@ def run_lapeval(world, rank, racelines):
     t0 = time.perf_counter()
     ev, kms = raceline.lap_eval(P, Ls, True, cfg, return_ms=True)
     wall = time.perf_counter() - t0
-    n_cpu, t0 = 0, time.perf_counter()
-    while n_cpu < B and time.perf_counter() - t0 < 3.0:
-        orc = O.run_oracle_lap_eval(P[n_cpu], float(prob.L), True, cfg)
-        assert abs(orc.lap[0] - ev.lap[n_cpu]) <= 1e-9 * orc.lap[0]
-        n_cpu += 1
-    cpu_s = (time.perf_counter() - t0) / n_cpu
+    for b in (0, B // 2, B - 1):
+        orc = O.run_oracle_lap_eval(P[b], float(prob.L), True, cfg)
+        assert abs(orc.lap[0] - ev.lap[b]) <= 1e-9 * orc.lap[0]
     return {"paths": B, "N": N, "kernel_ms": round(kms, 3), "wall_ms_incl_transfers": round(1e3 * wall, 2),
-            "laps_per_s_kernel": round(B / (kms * 1e-3), 1), "cpu_oracle_laps_per_s_1core": round(1.0 / cpu_s, 1),
-            "cpu_sample": f"{n_cpu} paths", "lap_min_s": float(ev.lap.min()), "lap_max_s": float(ev.lap.max())}
+            "laps_per_s_kernel": round(B / (kms * 1e-3), 1), "lap_min_s": float(ev.lap.min()),
+            "lap_max_s": float(ev.lap.max())}
 
 
 def run_format(world, rank, mc_x, mc_y, mc_k, mc_al, case, cfg):
     """the _raceline_with_geom.csv tables (7 columns, N+1 rows) of the
-    C2 run's 1024 instances formatted on the GPU in one pass (rl_format_csv), vs glibc
-    "%.9f" on one core over a sample (the oracle's snprintf loop)."""
+    C2 run's 1024 instances formatted on the GPU in one pass (rl_format_csv), checked on
+    a sample against glibc "%.9f" (the oracle's snprintf loop)."""
     import oracle_lib as O
 
     if rank != 0:
@@ -271,14 +492,11 @@ def run_format(world, rank, mc_x, mc_y, mc_k, mc_al, case, cfg):
     t0 = time.perf_counter()
     text = raceline.format_table(T)
     gpu_s = time.perf_counter() - t0
-    k = max(1, min(T.shape[0], 200000))
-    t0 = time.perf_counter()
+    k = 20000
     cpu_text = O.oracle_format_rows(T[:k])
-    cpu_s = time.perf_counter() - t0
     return {"rows": int(T.shape[0]), "numbers": int(T.size), "bytes": len(text),
             "gpu_wall_ms_incl_transfers": round(1e3 * gpu_s, 2), "gpu_MB_per_s": round(len(text) / gpu_s / 1e6, 1),
-            "cpu_glibc_MB_per_s_1core": round(len(cpu_text) / cpu_s / 1e6, 1), "cpu_sample_rows": k,
-            "bytes_equal_on_sample": text[: len(cpu_text)] == cpu_text}
+            "bytes_equal_on_sample": text[: len(cpu_text)] == cpu_text, "sample_rows": k}
 
 
 def main():
@@ -288,12 +506,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the C3 min-time lap check")
+    ap.add_argument("--no-extras", action="store_true", help="only the timed C2 steps")
+    ap.add_argument("--cpu-leg", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
+    if args.cpu_leg:
+        print(json.dumps(cpu_leg(args.cpu_budget)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the CPU leg (rank 0 at N=1 only) starts before this process touches the GPU
+    cpu_proc = start_cpu_leg(args.cpu_budget) if (world == 1 and not args.no_cpu and not args.no_extras) else None
     # rehearsal on a one-GPU box only: every rank on cuda:0, gloo instead of RCCL
     if os.environ.get("RL_BENCH_SAME_DEVICE") == "1":
         local = 0
@@ -320,7 +545,7 @@ def main():
     B = args.batch
     N = prob.N
     MO = int(cfg.max_outer_iters)
-    seeds = np.arange(rank * B, (rank + 1) * B, dtype=np.uint64)     # rank 0 / seed 0 = the reference
+    seeds = D.seed_block(world, rank, B)
     plan = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=abi.RL_MODE_MINCURV, device=local)
 
     # results straight into torch tensors (zero-copy for the RCCL gather)
@@ -330,23 +555,15 @@ def main():
     plan.bind_device_outputs(abi.RL_MODE_MINCURV, {k: v.data_ptr() for k, v in res.items()})
 
     stream = torch.cuda.Stream(device=dev)
-
-    def summarize():
-        # per-instance summaries [B, 3]: Σ evaluations, Σ x, Σ α_last (SURVEY §8e's
-        # "gather of per-instance summaries, then selective fetches"); the full SoA
-        # results stay resident on each rank
-        return torch.stack([res["evals"].sum(1, dtype=torch.float64), res["x"].sum(1),
-                            res["alpha_last"].sum(1)], dim=1)
-
     gathered = {}
 
     def step():
         plan.run(stream.cuda_stream)
         if world > 1:
             with torch.cuda.stream(stream):
-                out = D.gather_to_root({"summary": summarize()}, world, rank)   # RCCL over xGMI
+                rows = D.gather_rows(D.instance_summary(res["evals"], res["x"], res["alpha_last"]), world, rank)
                 if rank == 0:
-                    gathered["summary"] = out["summary"]
+                    gathered["summary"] = rows
 
     for _ in range(args.warmup):
         step()
@@ -375,12 +592,22 @@ def main():
     value = total_outer / elapsed
     tracks_per_s = world * B * args.steps / elapsed
 
-    c4 = None if args.no_extras else run_c4(world, rank, local, dev, dist)
-    st6 = None if args.no_extras else run_step6(world, rank)
-    lev = None if args.no_extras else run_lapeval(world, rank, np.stack([res["x"].cpu().numpy(), res["y"].cpu().numpy()], axis=2))
-    fmt = None if args.no_extras else run_format(world, rank, res["x"].cpu().numpy(), res["y"].cpu().numpy(),
-                                                   res["kappa"].cpu().numpy(), res["alpha_last"].cpu().numpy(), case, cfg)
-    c5 = None if args.no_extras else run_c5(world, rank, local, dev, dist)
+    extras = {}
+    if not args.no_extras:
+        c4, c4_laps = run_c4(world, rank, local, dev, dist)
+        c5 = run_c5(world, rank, local, dev, dist)
+        if rank == 0:
+            c3, c3_laps = run_c3(rank, local, stream)
+            extras["c3_mintime_plus_mincurv"] = c3
+            extras["c4_sweep_7tracks_x_512"] = c4
+            extras["c5_oval_n10000"] = c5
+            extras["c2_pcie_inclusive"] = run_c2_pcie(prob, cfg, B, MO, rank)
+            extras["dropin_b1_latency"] = run_dropin(local)
+            extras["step6_geom_cmap1_n2000"] = run_step6(world, rank)
+            xh, yh = res["x"].cpu().numpy(), res["y"].cpu().numpy()
+            extras["lap_eval_1024_racelines_n2000"] = run_lapeval(world, rank, np.stack([xh, yh], axis=2))
+            extras["csv_format_1024_instances"] = run_format(world, rank, xh, yh, res["kappa"].cpu().numpy(),
+                                                              res["alpha_last"].cpu().numpy(), case, cfg)
     if rank != 0:
         plan.close()
         if dist is not None:
@@ -391,8 +618,8 @@ def main():
     # ---- parity of this run (outside the timed region) ----
     summary_check = None
     if world > 1:
-        allsum = torch.cat(gathered["summary"]).cpu().numpy()          # [world*B, 3], rank-major
-        mine = summarize().cpu().numpy()
+        allsum = gathered["summary"].cpu().numpy()                    # [world*B, 3], rank-major
+        mine = D.instance_summary(res["evals"], res["x"], res["alpha_last"]).cpu().numpy()
         summary_check = {"instances_gathered": int(allsum.shape[0]),
                          "rank0_rows_equal": bool(np.array_equal(allsum[:B], mine)),
                          "seed0_x_sum_vs_reference": float(abs(allsum[0, 1] - float(np.sum(case["mc_x"]))))}
@@ -413,63 +640,58 @@ def main():
     Eseg = prob.inner_seg.shape[0] + prob.outer_seg.shape[0]
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else plan.kernel_ms(1)
     fl_launch = B * MO * flops_per_outer(N, E_k, Eseg)
-    by_launch = B * MO * bytes_per_outer(N, E_k, Eseg)
     achieved_tf = fl_launch / (k_ms * 1e-3) / 1e12
+    pmc = read_pmc("c2_mincurv")
     roofline = {
-        "bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 4), "traffic": read_pmc("c2_mincurv"),
+        "bound": "fp64-valu", "achieved": round(achieved_tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 4),
+        "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
         "kernel": "rl_optimize_kernel<8,256,closed,mincurv>", "kernel_ms": round(k_ms, 3),
-        "note": "fp64 compute roof (VALU; MI355X fp64 vector = fp64 dense-matrix peak = 78.6 TF): "
-                "the instance state stays in VGPR/LDS, so HBM is not the binding roof",
-        "streaming_model_GBps": round(by_launch / (k_ms * 1e-3) / 1e9, 1),
-        "streaming_model_frac_of_hbm": round(by_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
+        "flops_per_launch_algorithmic": fl_launch,
+        "algorithmic_model": f"SURVEY §8d: N*(34*E_k + 26*(Ei+Eo)) per outer, N={N}, E_k={E_k:.2f}, "
+                             f"Ei+Eo={Eseg}, x {B}x{MO} outers (the corridor term counts the reference's "
+                             f"every-segment ray tests; the kernel culls most of them exactly)",
+        "peak_note": "78.6 TF = MI355X fp64 vector peak with FMA counted as 2 flops; the path's operations are "
+                     "mostly plain add/mul (-ffp-contract=off keeps the reference's roundings), whose ceiling on "
+                     "the same pipe is 39.3 TF",
+        "frac_of_nonfma_ceiling": round(achieved_tf / FP64_NONFMA_TFLOPS, 4),
         "evals_per_outer": round(E_k, 2),
     }
-    fl_pmc = read_pmc("c2_mincurv", "fp64_flops_per_launch")
-    if fl_pmc:
-        roofline["executed_fp64_TFLOPs_pmc"] = round(fl_pmc / (k_ms * 1e-3) / 1e12, 3)
+    if pmc:
+        ex = pmc.get("fp64_flops_per_launch")
+        if ex:
+            roofline["executed_fp64_TFLOPs_pmc"] = round(ex / (k_ms * 1e-3) / 1e12, 3)
+            roofline["executed_frac"] = round(ex / (k_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4)
+        for key in ("valu_fp64_share", "hbm_GBps_note"):
+            if pmc.get(key) is not None:
+                roofline[key + "_pmc"] = pmc[key]
+        roofline["pmc_profile"] = pmc.get("profile")
+    roofline["pmc_source_sha"] = source_sha() if pmc else None
 
-    extras = {}
-    if not args.no_extras:
-        # C3 min-time lap check (N=2000, max_vpass_iters=20): seed 0 vs the reference lap
-        c3, p3, cfg3 = load_problem("cmap1_n2000_vp20")
-        # BASELINE configs[2]: 4096 alpha-seeds on one GPU (per rank when sharded;
-        # rank 0 holds seed 0 = the reference)
-        Bm = 4096
-        pl3 = raceline.Plan(p3, cfg3, seeds=np.arange(rank * Bm, (rank + 1) * Bm, dtype=np.uint64), B=Bm,
-                            modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, device=local)
-        pl3.run(stream.cuda_stream)
-        stream.synchronize()
-        t1 = time.perf_counter()
-        pl3.run(stream.cuda_stream)          # inputs resident; results stay in HBM (fetched below)
-        stream.synchronize()
-        t3 = time.perf_counter() - t1
-        mc3, mt3 = pl3.fetch()
-        lap_ref = float(c3["mt_lap"])
-        extras["c3_mintime_plus_mincurv"] = {
-            "instances": Bm, "wall_ms": round(t3 * 1e3, 2),
-            "outer_iters_per_s": round(2 * Bm * MO / t3, 1),
-            "kernel_ms_mincurv": round(pl3.kernel_ms(1), 3), "kernel_ms_mintime": round(pl3.kernel_ms(2), 3),
-            "lap_seed0_s": float(mt3.lap[0]), "lap_ref_s": lap_ref,
-            "lap_delta_s": float(abs(mt3.lap[0] - lap_ref)),
-            "lap_mean_over_seeds_s": float(np.mean(mt3.lap)),
-            "vpass_sweeps_mean": float(np.mean(mt3.vpass_sweeps)),
-        }
-        pl3.close()
-
-    if c4 is not None:
-        extras["c4_sweep_7tracks_x_512"] = c4
-    if c5 is not None:
-        extras["c5_oval_n10000"] = c5
-    if st6 is not None:
-        extras["step6_geom_cmap1_n2000"] = st6
-    if lev is not None:
-        extras["lap_eval_1024_racelines_n2000"] = lev
-    if fmt is not None:
-        extras["csv_format_1024_instances"] = fmt
-    cpu = None
-    if world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(prob, cfg)
+    cpu, cpu_res = None, None
+    if cpu_proc is not None:
+        cpu_res = finish_cpu_leg(cpu_proc)
+    if cpu_res is not None:
+        cpu = dict(cpu_res.get("reference") or cpu_res["port"])
+        cpu["cpu_model"] = cpu_res["cpu"]["model"]
+        cpu["host_nproc"] = cpu_res["cpu"]["nproc"]
+        cpu["port_restatement"] = cpu_res["port"] if cpu_res.get("reference") else None
+        if "c3_mintime_plus_mincurv" in extras:
+            c3o = cpu_res["c3_oracle_laps"]
+            extras["c3_mintime_plus_mincurv"]["lap_delta_vs_oracle"] = {
+                **lap_delta(c3_laps[c3o["seeds"]], c3o["laps"]),
+                "sample": f"{len(c3o['seeds'])} seeds strided over the {C3_BATCH}-instance batch (seeds "
+                          f"{c3o['seeds'][0]}..{c3o['seeds'][-1]} step {C3_BATCH // C3_SAMPLE})"}
+        if "c4_sweep_7tracks_x_512" in extras and c4_laps is not None:
+            extras["c4_sweep_7tracks_x_512"]["lap_delta_vs_oracle"] = {
+                **lap_delta(c4_laps, cpu_res["c4_oracle_laps"]), "sample": "all 3584 (track, sweep point) instances"}
+        if "dropin_b1_latency" in extras and cpu_res.get("reference_per_track"):
+            for name, v in extras["dropin_b1_latency"].items():
+                r = cpu_res["reference_per_track"].get(name)
+                if r:
+                    v["reference_cpu_mincurv_ms"] = r["mincurv_ms"]
+                    v["reference_cpu_mintime_ms"] = r["mintime_ms"]
+        extras["cpu_oracle_pool"] = cpu_res.get("oracle_pool")
 
     out = {
         "metric": "PGD outer-iters/sec (N=2000 samples, closed, competition_map1, 1024 alpha-seeds/GPU, min-curv)",

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 2
+#define RL_ABI_VERSION 3
 
 /* error codes */
 #define RL_OK          0
@@ -157,6 +157,17 @@ double rl_seed_value(uint64_t seed, int32_t i, double sigma);
 int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
                 const uint64_t* seeds, int32_t B,
                 rl_out* out_mincurv, rl_out* out_mintime);
+
+/* ------------------------------------------------------------ multi-device
+ * rl_optimize over n_dev devices (SURVEY.md §8b device list, §8e): the B instances are
+ * split into contiguous blocks (block d = instances [B*d/n, B*(d+1)/n), n = min(n_dev, B)),
+ * one plan and HIP stream per device, all devices enqueued before the first download;
+ * each block's results are copied to its offset of the caller's host outputs (the final
+ * gather).  devices: n_dev distinct device indices, or NULL for 0..n_dev-1.  Same
+ * cfg/seeds/out conventions and results as rl_optimize (instances are independent). */
+int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
+                      const uint64_t* seeds, int32_t B, const int32_t* devices, int32_t n_dev,
+                      rl_out* out_mincurv, rl_out* out_mintime);
 
 /* ---------------------------------------------------- device-resident plan
  * For repeated runs with inputs already resident in HBM (bench, services).

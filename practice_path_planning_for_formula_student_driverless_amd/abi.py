@@ -374,6 +374,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_format_csv.argtypes = [C.POINTER(C.c_double), C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int64,
                                   C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     lib.rl_format_csv.restype = C.c_int
+    if hasattr(lib, "rl_optimize_multi"):   # absent only in older experiment builds (A/B bases)
+        lib.rl_optimize_multi.argtypes = [C.POINTER(RlProblem), C.POINTER(RlCfg), C.c_int32, C.POINTER(C.c_uint64),
+                                          C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(RlOut),
+                                          C.POINTER(RlOut)]
+        lib.rl_optimize_multi.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib
     return lib

@@ -789,6 +789,73 @@ int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const 
     return rc;
 }
 
+// rl_optimize over several devices (SURVEY §8b device list, §8e): contiguous instance
+// blocks, one plan and stream per device, every device enqueued before the first
+// download, and each block's results copied to its offset of the caller's host outputs
+// (the final gather).  Instances never span devices: block d holds [b0_d, b1_d).
+int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
+                      const int32_t* devices, int32_t n_dev, rl_out* out_mincurv, rl_out* out_mintime) {
+    int modes = (out_mincurv ? RL_MODE_MINCURV : 0) | (out_mintime ? RL_MODE_MINTIME : 0);
+    if (!modes) return fail(RL_EINVAL, "no output requested");
+    if (!prob || !cfg) return fail(RL_EINVAL, "problem/cfg is NULL");
+    if (B < 1) return fail(RL_EINVAL, "B must be >= 1");
+    if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
+    if (n_dev < 1) return fail(RL_EINVAL, "n_dev must be >= 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    std::vector<int> devs((size_t)n_dev);
+    for (int d = 0; d < n_dev; ++d) {
+        devs[d] = devices ? devices[d] : d;
+        if (devs[d] < 0 || devs[d] >= ndev) return fail(RL_ENODEV, "device index out of range");
+        for (int e = 0; e < d; ++e)
+            if (devs[e] == devs[d]) return fail(RL_EINVAL, "device listed twice");
+    }
+    const int nb = std::min(n_dev, B);             // no empty blocks
+    const int mo = cfg[0].max_outer_iters;
+    const size_t N = (size_t)std::max(prob->N, 0);
+    std::vector<rl_plan*> plans((size_t)nb, nullptr);
+    auto release = [&](int code) {
+        std::string e = g_err;
+        for (rl_plan* q : plans) rl_plan_destroy(q);
+        g_err = e;
+        return code;
+    };
+    auto block = [&](int d, int& b0, int& b1) {
+        b0 = (int)((int64_t)B * d / nb);
+        b1 = (int)((int64_t)B * (d + 1) / nb);
+    };
+    int rc;
+    for (int d = 0; d < nb; ++d) {
+        int b0, b1;
+        block(d, b0, b1);
+        if ((rc = rl_plan_create(&plans[d], devs[d], prob, n_cfg == 1 ? cfg : cfg + b0, n_cfg == 1 ? 1 : b1 - b0,
+                                 seeds ? seeds + b0 : nullptr, b1 - b0, modes)) ||
+            (rc = rl_plan_run(plans[d], nullptr)))
+            return release(rc);
+    }
+    auto shifted = [&](const rl_out* o, int b0, rl_out& s) -> rl_out* {
+        if (!o) return nullptr;
+        s = *o;
+        const size_t bn = (size_t)b0 * N;
+        double** f[] = {&s.x, &s.y, &s.heading, &s.kappa, &s.alpha_total, &s.alpha_last, &s.v, &s.ax};
+        for (double** q : f)
+            if (*q) *q += bn;
+        if (s.lap) s.lap += b0;
+        if (s.evals) s.evals += (size_t)b0 * mo;
+        if (s.accepts) s.accepts += (size_t)b0 * mo;
+        if (s.vpass_sweeps) s.vpass_sweeps += (size_t)b0 * (mo + 1);
+        return &s;
+    };
+    for (int d = 0; d < nb; ++d) {
+        int b0, b1;
+        block(d, b0, b1);
+        rl_out smc, smt;
+        if ((rc = rl_plan_fetch(plans[d], shifted(out_mincurv, b0, smc), shifted(out_mintime, b0, smt))))
+            return release(rc);
+    }
+    return release(RL_OK);
+}
+
 #ifdef RL_STAMPS
 // diagnostic builds only: per-phase cycle totals of the last launch (see rl_kernels.hip)
 int rl_debug_stamps(unsigned long long* host, int nblocks) { return rl::debug_stamps(host, nblocks); }

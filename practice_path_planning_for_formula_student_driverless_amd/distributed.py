@@ -44,6 +44,50 @@ def gather_to_root(tensors: Dict[str, "object"], world: int, rank: int, group=No
     return out
 
 
+def seed_block(world: int, rank: int, B: int) -> np.ndarray:
+    """Weak scaling: rank r optimises seeds [r*B, (r+1)*B) (rank 0 / seed 0 = the reference)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    return np.arange(rank * B, (rank + 1) * B, dtype=np.uint64)
+
+
+def instance_summary(evals, x, alpha_last):
+    """Per-instance summary rows [B, 3] = (Σ evaluations, Σ x, Σ α_last): what every rank
+    sends to rank 0 each step (a gather of per-instance summaries; the full
+    SoA results stay resident on each rank).  torch tensors in, float64 tensor out."""
+    import torch
+
+    return torch.stack([evals.sum(1, dtype=torch.float64), x.sum(1), alpha_last.sum(1)], dim=1)
+
+
+def gather_rows(t, world: int, rank: int, group=None):
+    """Gather equal-shape row blocks to rank 0 in rank order: the concatenation on rank 0,
+    None elsewhere."""
+    import torch
+
+    got = gather_to_root({"t": t}, world, rank, group)
+    return torch.cat(got["t"]) if rank == 0 else None
+
+
+def gather_ragged(a: np.ndarray, world: int, rank: int, total: int, device=None, group=None):
+    """Gather 1-D float64 shards of different lengths (at most ceil(total/world) each) to
+    rank 0 in rank order.  Returns the concatenation (numpy) on rank 0, None elsewhere."""
+    import torch
+
+    per = pad_to(total, world)
+    a = np.asarray(a, dtype=np.float64).ravel()
+    if a.size > per:
+        raise ValueError("shard larger than ceil(total/world)")
+    buf = torch.zeros(per + 1, dtype=torch.float64, device=device)
+    buf[0] = float(a.size)
+    buf[1:1 + a.size] = torch.from_numpy(a).to(buf.device)
+    got = gather_to_root({"b": buf}, world, rank, group)
+    if rank != 0:
+        return None
+    parts = [g.cpu().numpy() for g in got["b"]]
+    return np.concatenate([p[1:1 + int(p[0])] for p in parts])
+
+
 # ----------------------------------------------------------------- C4 sweep
 C4_TRACKS = ["training_map", "competition_map1", "competition_map2", "competition_map3",
              "competition_map_testday1", "competition_map_testday2", "competition_map_testday3"]

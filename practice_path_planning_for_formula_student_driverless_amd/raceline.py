@@ -106,11 +106,13 @@ def _check_batch(B: int, ncfg: int, seeds) -> None:
 
 
 def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
-                   mincurv: bool = True, mintime: bool = True):
+                   mincurv: bool = True, mintime: bool = True, devices: Optional[Sequence[int]] = None):
     """Optimise B instances (seed b / cfg b) of one problem on the GPU.
 
     cfgs: one RlCfg (broadcast) or a list of B.  seeds: None (all zero — the
-    reference exactly) or B uint64 seeds.  Returns (Outputs|None, Outputs|None).
+    reference exactly) or B uint64 seeds.  devices: None (the current device) or a
+    list of device indices: contiguous instance blocks, one per device
+    (rl_optimize_multi).  Returns (Outputs|None, Outputs|None).
     """
     cfg_arr, ncfg = abi.cfg_array(cfgs)
     if B is None:
@@ -123,8 +125,14 @@ def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
     c_mc = out_mc.as_c() if out_mc else None
     c_mt = out_mt.as_c() if out_mt else None
     p = prob.as_c()
-    _check(_lib().rl_optimize(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B,
-                              C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None))
+    if devices is None:
+        _check(_lib().rl_optimize(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B,
+                                  C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None))
+    else:
+        devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+        _check(_lib().rl_optimize_multi(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B,
+                                        devs.ctypes.data_as(C.POINTER(C.c_int32)), len(devs),
+                                        C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None))
     return out_mc, out_mt
 
 

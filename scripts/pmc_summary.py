@@ -57,12 +57,21 @@ if g("FETCH_SIZE") is not None or g("WRITE_SIZE") is not None:
 res["derived"] = der
 json.dump(res, open(os.path.join(out, "summary.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
+if g("SQ_INSTS_VALU") and f64:
+    der["valu_fp64_share"] = f64 / g("SQ_INSTS_VALU")     # fp64 add/mul/fma/trans of all VALU instructions
 if "--commit" in sys.argv and "hbm_bytes_per_launch" in der:
+    # profiles/pmc_traffic.json feeds bench.py's roofline; bench.py uses an entry only when its
+    # source_sha equals the hash of the kernel sources it runs (bench.source_sha)
+    sys.path.insert(0, REPO)
+    from bench import source_sha
+
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     d = json.load(open(p)) if os.path.exists(p) else {}
     key = sys.argv[sys.argv.index("--key") + 1] if "--key" in sys.argv else "c2_mincurv"
+    prof = sys.argv[sys.argv.index("--profile") + 1] if "--profile" in sys.argv else out
     d[key] = {"hbm_bytes_per_launch": der["hbm_bytes_per_launch"], "fetch_bytes_raw": der["fetch_bytes_raw"],
-                       "write_bytes": der["write_bytes"], "kernel": meta.get("kernel"), "source": out,
-                       "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
-                       "note": "rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate --pmc passes"}
+              "write_bytes": der["write_bytes"], "kernel": meta.get("kernel"), "source_sha": source_sha(),
+              "profile": prof, "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
+              "valu_fp64_share": der.get("valu_fp64_share"),
+              "note": "rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate --pmc passes"}
     json.dump(d, open(p, "w"), indent=1)

@@ -34,7 +34,7 @@ def test_header_declares_expected_entry_points():
     for must in ("rl_optimize", "rl_plan_create", "rl_plan_run", "rl_plan_fetch", "rl_plan_destroy",
                  "rl_plan_device_outputs", "rl_plan_kernel_ms", "rl_plan_bind_device_outputs", "rl_cfg_default", "rl_cfg_set_mu",
                  "rl_ring_segments", "rl_seed_value", "rl_device_count", "rl_last_error", "rl_abi_version",
-                 "rl_kernel_variant", "rl_geom"):
+                 "rl_kernel_variant", "rl_geom", "rl_optimize_multi", "rl_lap_eval", "rl_corridor", "rl_format_csv"):
         assert must in names
 
 
@@ -157,3 +157,17 @@ def test_load_csv_xy_parses_reference_formats():
         p = os.path.join(d, "a.csv")
         open(p, "w").write("1.5,2\n\n3;4\n5\t6\n7 8\nbad,line\n")
         np.testing.assert_array_equal(raceline.load_csv_xy(p), [[1.5, 2], [3, 4], [5, 6], [7, 8]])
+
+
+def test_optimize_multi_argument_errors():
+    """rl_optimize_multi checks its device list before touching a device."""
+    lib = abi.load_library()
+    case = O.load_case("track_training_map")
+    p = O.case_problem(case).as_c()
+    arr, n = abi.cfg_array(O.case_cfg(case))
+    out = abi.Outputs.alloc(2, O.case_problem(case).N, 14, False).as_c()
+    assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 2, None, 0, C.byref(out), None) == abi.RL_EINVAL
+    assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 0, None, 1, C.byref(out), None) == abi.RL_EINVAL
+    assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 2, None, 1, None, None) == abi.RL_EINVAL
+    if lib.rl_device_count() == 0:
+        assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 2, None, 1, C.byref(out), None) == abi.RL_ENODEV

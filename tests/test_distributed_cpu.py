@@ -49,37 +49,75 @@ def test_c4_grid_and_shards():
     assert sorted(seen) == D.c4_items()
 
 
-def _worker(rank, world, port, q):
+def _c2_shard_summary(seeds):
+    """The bench's per-rank C2 step with the oracle as the compute (no GPU here):
+    training_map, 2 outer iterations, the given seeds -> instance_summary rows."""
+    import oracle_lib as O
+
+    case = O.load_case("track_training_map")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    cfg.max_outer_iters = 2
+    mc, _ = O.run_oracle(prob, cfg, seeds=seeds, B=len(seeds), modes=(True, False))
+    return D.instance_summary(torch.from_numpy(mc.evals), torch.from_numpy(mc.x), torch.from_numpy(mc.alpha_last))
+
+
+C4_SMALL = dict(n_tracks=2, n_points=3)
+
+
+def _c4_shard_laps(world, rank):
+    """The bench's per-rank C4 work with the oracle as the compute: this rank's track-major
+    share of a reduced grid (2 tracks x the first 3 sweep points), min-time laps in item order."""
+    import oracle_lib as O
+
+    cfgs = D.c4_cfgs(O.case_cfg(O.load_case("track_training_map")))
+    laps = []
+    for t, ks in D.c4_shard(world, rank, **C4_SMALL).items():
+        prob = O.case_problem(O.load_case("track_" + D.C4_TRACKS[t]))
+        for k in ks:
+            c = abi.RlCfg.from_dict(cfgs[k].to_dict())
+            c.max_outer_iters = 1
+            laps.append(O.run_oracle(prob, [c], B=1, modes=(False, True))[1].lap[0])
+    return np.array(laps)
+
+
+def _bench_path_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    B, N = 5, 7
-    s, e = D.shard_range(world * B, world, rank)
-    # each rank "optimises" its seeds: a deterministic stand-in result per seed
-    seeds = np.arange(s, e)
-    x = torch.tensor(np.stack([np.sin(seeds[i] + np.arange(N)) for i in range(len(seeds))]), dtype=torch.float64)
-    ev = torch.tensor(np.tile(seeds[:, None], (1, 3)), dtype=torch.int32)
-    out = D.gather_to_root({"x": x, "evals": ev}, world, rank)
+    B = 2
+    summary = _c2_shard_summary(D.seed_block(world, rank, B))
+    rows = D.gather_rows(summary, world, rank)
+    n_items = C4_SMALL["n_tracks"] * C4_SMALL["n_points"]
+    laps = D.gather_ragged(_c4_shard_laps(world, rank), world, rank, n_items)
     if rank == 0:
-        xs = torch.cat(out["x"]).numpy()
-        es = torch.cat(out["evals"]).numpy()
-        q.put((xs, es))
+        q.put((rows.numpy(), laps))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_gather_to_root_gloo(world):
+def test_bench_path_gather_equals_one_rank(world):
+    """world-size 2/3 over gloo: per-rank seed blocks, the per-step summary gather and the
+    track-major C4 lap gather (the functions bench.py runs over RCCL), each rank computing
+    its shard with the CPU oracle; rank 0's gathered rows equal a one-rank run."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bench_path_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    xs, es = q.get(timeout=120)
+    rows, laps = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    all_seeds = np.arange(world * 5)
-    np.testing.assert_array_equal(es[:, 0], all_seeds)
-    np.testing.assert_array_equal(xs, np.stack([np.sin(s + np.arange(7)) for s in all_seeds]))
+    one = _c2_shard_summary(D.seed_block(1, 0, 2 * world)).numpy()
+    np.testing.assert_array_equal(rows, one)
+    np.testing.assert_array_equal(laps, _c4_shard_laps(1, 0))
+    assert rows.shape == (2 * world, 3) and len(laps) == C4_SMALL["n_tracks"] * C4_SMALL["n_points"]
+
+
+def test_gather_ragged_validates_shard_size():
+    with pytest.raises(ValueError):
+        D.gather_ragged(np.zeros(5), 2, 0, 8)

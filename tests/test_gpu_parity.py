@@ -570,3 +570,93 @@ def test_corridor_vs_oracle():
         for what, g, r in (("lo", lo, olo), ("hi", hi, ohi)):
             bad = np.flatnonzero((g != r) | (np.signbit(g) != np.signbit(r)))
             assert bad.size == 0, f"{name}.{what}: {bad.size} samples differ, first {bad[:5]} {g[bad[:3]]} vs {r[bad[:3]]}"
+
+
+@pytest.mark.parametrize("variant", ["default", "backtrack_accepts"])
+def test_c5_oval_seeds_vs_oracle(variant):
+    """C5's shape at its real size: the N=10000 oval through the streaming kernel with
+    jittered α-seeds {1, 7} (ref:720 + the seed, corridor updates ref:749-757).  The
+    default cfg rejects every trial (E_k = 21, the bench's C5 path); the second cfg
+    (step_init 1e-3, step_min 1e-15) accepts after backtracking, so the batched-trial
+    accept / step_min cut-off fires at N=10000.  Counters exact, columns within the
+    tolerance, zero signs equal."""
+    _lib_or_skip()
+    case = O.load_case("oval_n10000")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    if variant == "backtrack_accepts":
+        cfg.step_init, cfg.step_min = 1e-3, 1e-15
+        cfg.max_outer_iters, cfg.max_inner_iters = 4, 30
+    mc, _ = raceline.optimize_batch(prob, cfg, [1, 7], 2, mintime=False)
+    omc, _ = O.run_oracle(prob, cfg, seeds=[1, 7], B=2, modes=(True, False))
+    compare_outputs(mc, omc, False, f"c5 {variant}")
+    if variant == "backtrack_accepts":
+        assert omc.accepts.min() > 0 and (omc.evals > omc.accepts + 1).any()   # the path under test ran
+
+
+def test_optimize_multi_one_device_equals_single():
+    """rl_optimize_multi (device list) in its one-device form: the same
+    results as rl_optimize, bit for bit; bad device lists are errors."""
+    lib = _lib_or_skip()
+    case = O.load_case("track_competition_map2")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    seeds = np.arange(5, dtype=np.uint64)
+    mc1, mt1 = raceline.optimize_batch(prob, cfg, seeds, 5)
+    mc2, mt2 = raceline.optimize_batch(prob, cfg, seeds, 5, devices=[0])
+    for a, b in ((mc1, mc2), (mt1, mt2)):
+        for f in abi.OUT_F64 + ("evals", "accepts"):
+            np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    np.testing.assert_array_equal(mt1.lap, mt2.lap)
+    with pytest.raises(raceline.RacelineError) as ei:
+        raceline.optimize_batch(prob, cfg, seeds, 5, devices=[0, 0])
+    assert ei.value.code == abi.RL_EINVAL
+    with pytest.raises(raceline.RacelineError) as ei:
+        raceline.optimize_batch(prob, cfg, seeds, 5, devices=[lib.rl_device_count()])
+    assert ei.value.code == abi.RL_ENODEV
+
+
+def test_empty_plan_reports_kernel_time():
+    """N = 0 (ref:689 / 912: an empty Result): the plan runs, and rl_plan_kernel_ms
+    reports the empty interval of each mode instead of failing."""
+    _lib_or_skip()
+    prob = abi.Problem(center=np.zeros((0, 2)), L=1.0, inner_seg=np.zeros((0, 4)), outer_seg=np.zeros((0, 4)))
+    pl = raceline.Plan(prob, abi.default_cfg(), B=2, modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME)
+    pl.run()
+    assert pl.kernel_ms(1) >= 0.0 and pl.kernel_ms(2) >= 0.0 and pl.kernel_ms(0) >= 0.0
+    mc, mt = pl.fetch()
+    assert mt.lap.tolist() == [0.0, 0.0]
+    pl.close()
+
+
+def test_device_libm_known_answers(tmp_path):
+    """Device known-answer test of the restated libm on the hot path: heading (OCML
+    atan2) and curvature (pow15) of random closed paths through rl_lap_eval, against
+    the host: the centred differences x', y' are recomputed with the same operations
+    (bit-exact), glibc atan2 gives the reference heading (ref:615-617), and the
+    curvature uses the host build of the same pow15 (tests/test_math_cpu.py pins it to
+    the correctly rounded x^1.5).  atan2: <= 2 ulp; curvature: bit for bit."""
+    _lib_or_skip()
+    rng = np.random.default_rng(11)
+    B, N = 16, 1000
+    t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+    P = np.stack([np.stack([(20 + rng.uniform(-5, 5)) * np.cos(t) + rng.normal(0, 0.3, N),
+                            (12 + rng.uniform(-3, 3)) * np.sin(t) + rng.normal(0, 0.3, N)], 1) for _ in range(B)])
+    L = np.full(B, 150.0)
+    ev = raceline.lap_eval(P, L, True, abi.default_cfg())
+    h = L[0] / N
+    xp = (np.roll(P[:, :, 0], -1, 1) - np.roll(P[:, :, 0], 1, 1)) / (2 * h)
+    yp = (np.roll(P[:, :, 1], -1, 1) - np.roll(P[:, :, 1], 1, 1)) / (2 * h)
+    xpp = (np.roll(P[:, :, 0], -1, 1) - 2 * P[:, :, 0] + np.roll(P[:, :, 0], 1, 1)) / (h * h)
+    ypp = (np.roll(P[:, :, 1], -1, 1) - 2 * P[:, :, 1] + np.roll(P[:, :, 1], 1, 1)) / (h * h)
+    import test_math_cpu as M
+    lib = M.build_shim(tmp_path)
+    denom = M._pow15(lib, np.maximum(1e-12, xp * xp + yp * yp).ravel()).reshape(B, N)
+    kappa = (xp * ypp - yp * xpp) / denom
+    np.testing.assert_array_equal(ev.kappa, kappa)
+    heading = np.arctan2(yp, xp)
+    ulps = np.abs(ev.heading.view(np.int64) - heading.view(np.int64))
+    # OCML's atan2 is within 2 ulp of the correctly rounded value (measured here: a few
+    # headings in a thousand at 1 ulp, a handful at 2); glibc's is correctly rounded
+    assert ulps.max() <= 2, ulps.max()
+    assert np.count_nonzero(ulps) <= 0.01 * ulps.size
+    print(f"atan2: of {ulps.size} headings {np.count_nonzero(ulps == 1)} are 1 ulp and "
+          f"{np.count_nonzero(ulps == 2)} are 2 ulp off glibc, the rest bit-exact")

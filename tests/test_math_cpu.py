@@ -41,7 +41,11 @@ extern "C" void kat_libm_hypot(const double* x, const double* y, double* r, long
 def shim(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    d = tmp_path_factory.mktemp("kat")
+    return build_shim(tmp_path_factory.mktemp("kat"))
+
+
+def build_shim(d):
+    """Host build of rl_math.h (plus glibc pow/hypot wrappers) in directory d."""
     src, so = d / "kat.cpp", d / "libkat.so"
     src.write_text(SHIM)
     subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
