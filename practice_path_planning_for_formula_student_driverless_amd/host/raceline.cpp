@@ -41,6 +41,9 @@
 //   --seeds B   optimise B α-seeds in one launch; writes <base>_batch_summary.csv
 //   --repeat R  time R launches of the batch; prints outer-iters/s
 //   --device D  HIP device
+//   --devices 0,1,...  shard the --seeds batch over these devices: contiguous instance
+//               blocks, one plan/stream per device, results gathered to the host
+//               (rl_optimize_multi; --repeat then times whole calls, PCIe included)
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -663,6 +666,7 @@ inline vector<Vec2> splineUniformResample(const vector<Vec2>& ordered, int sampl
 // ============================ ABI glue ======================================
 namespace gpu {
 inline int device = 0;
+inline vector<int32_t> devices;   // --devices: a batch sharded over these (rl_optimize_multi)
 inline void check(int rc, const char* what) {
     if (rc < 0) throw std::runtime_error(string(what) + ": " + rl_last_error());
 }
@@ -1189,9 +1193,6 @@ static void batch_and_save(const string& base, const vector<Vec2>& center, doubl
     rl_cfg c = cfg::to_abi(C);
     vector<uint64_t> seeds(B);
     for (int b = 0; b < B; ++b) seeds[b] = (uint64_t)b;
-    rl_plan* plan = nullptr;
-    gpu::check(rl_plan_create(&plan, gpu::device, &pk.prob, &c, 1, seeds.data(), B, modes), "rl_plan_create");
-    gpu::check(rl_plan_run(plan, nullptr), "rl_plan_run");
     const size_t BN = (size_t)B * center.size();
     vector<double> lap(B), al(BN), x(BN), y(BN);
     vector<int32_t> ev((size_t)B * C.max_outer_iters);
@@ -1200,7 +1201,29 @@ static void batch_and_save(const string& base, const vector<Vec2>& center, doubl
     o.x = x.data(); o.y = y.data(); o.alpha_last = al.data(); o.evals = ev.data();
     const bool mt = modes & RL_MODE_MINTIME;
     if (mt) o.lap = lap.data();
-    gpu::check(rl_plan_fetch(plan, mt ? nullptr : &o, mt ? &o : nullptr), "rl_plan_fetch");
+    rl_plan* plan = nullptr;
+    if (!gpu::devices.empty()) {
+        // sharded over the listed devices (one mode per call: the summary reads one)
+        auto call = [&]() {
+            gpu::check(rl_optimize_multi(&pk.prob, &c, 1, seeds.data(), B, gpu::devices.data(),
+                                         (int32_t)gpu::devices.size(), mt ? nullptr : &o, mt ? &o : nullptr),
+                       "rl_optimize_multi");
+        };
+        call();
+        if (repeat > 0) {
+            auto t0 = std::chrono::steady_clock::now();
+            for (int r = 0; r < repeat; ++r) call();
+            double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            std::cerr << "[batch] B=" << B << " over " << gpu::devices.size() << " devices, " << repeat
+                      << " calls " << wall * 1e3 << " ms (PCIe included) -> "
+                      << (double)B * C.max_outer_iters * repeat / wall << " PGD outer-iters/s\n";
+        }
+        repeat = 0;
+    } else {
+        gpu::check(rl_plan_create(&plan, gpu::device, &pk.prob, &c, 1, seeds.data(), B, modes), "rl_plan_create");
+        gpu::check(rl_plan_run(plan, nullptr), "rl_plan_run");
+        gpu::check(rl_plan_fetch(plan, mt ? nullptr : &o, mt ? &o : nullptr), "rl_plan_fetch");
+    }
     if (repeat > 0) {
         auto t0 = std::chrono::steady_clock::now();
         for (int r = 0; r < repeat; ++r) gpu::check(rl_plan_run(plan, nullptr), "rl_plan_run");
@@ -1211,7 +1234,7 @@ static void batch_and_save(const string& base, const vector<Vec2>& center, doubl
         std::cerr << "[batch] B=" << B << " last run " << ms << " ms, " << repeat << " runs " << wall * 1e3
                   << " ms -> " << outers * repeat / wall << " PGD outer-iters/s\n";
     }
-    rl_plan_destroy(plan);
+    if (plan) rl_plan_destroy(plan);
     io::Csv fo(base + "_batch_summary.csv");
     fo.f << "seed,lap_time_s,mean_abs_alpha_last,evals_total\n";
     for (int b = 0; b < B; ++b) {
@@ -1363,6 +1386,11 @@ int main(int argc, char** argv) {
             else if (a == "--seeds") B = std::stoi(next());
             else if (a == "--repeat") repeat = std::stoi(next());
             else if (a == "--device") gpu::device = std::stoi(next());
+            else if (a == "--devices") {
+                std::stringstream ss(next());
+                string tok;
+                while (std::getline(ss, tok, ',')) gpu::devices.push_back(std::stoi(tok));
+            }
             else if (a == "--stop-after") stop_after = next();
             else if (a == "--set") {
                 const string kv = next();

@@ -23,9 +23,10 @@ VARIANTS = {
     "sts512": {"RL_STS": 512},
     "sts256": {"RL_STS": 256},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
+    "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }
 if __name__ == "__main__":
-    names = sys.argv[1:] or [n for n in VARIANTS if n != "stamps"]
+    names = sys.argv[1:] or [n for n in VARIANTS if n not in ("stamps", "count")]
     import shutil; shutil.rmtree(os.path.join(B.LIB_DIR, "variants"), ignore_errors=True)
     with ThreadPoolExecutor(4) as ex:
         for p in ex.map(lambda n: B.build_variant(n, VARIANTS[n]), names):

@@ -152,3 +152,21 @@ def test_full_cli_matches_reference(name, tmp_path):
         if name in BYTE_EXACT_ALL:
             assert files[key] == ref[key], f"{name}/{key}: {_first_diff(files[key], ref[key])}"
     assert "[mintime] Estimated laptime:" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_seed_batch_over_device_list(tmp_path):
+    """fsd_raceline's batch mode (--seeds B) through one plan and through rl_optimize_multi
+    (--devices 0, the device-list form): the same per-instance summary rows."""
+    name = OK_CASES[0]
+    r, _ = _run(name, tmp_path)
+    assert r.returncode == 0, r.stderr
+    cen = str(tmp_path / "t_centerline.csv")
+    rows = {}
+    for tag, extra in (("plan", []), ("multi", ["--devices", "0"])):
+        r2 = subprocess.run([_exe(), cen, "--seeds", "6", "--mode", "mintime", *extra], stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True, timeout=120)
+        assert r2.returncode == 0, r2.stderr
+        rows[tag] = (tmp_path / "t_centerline_batch_summary.csv").read_text()
+    assert rows["plan"] == rows["multi"]
+    assert len(rows["plan"].splitlines()) == 7
