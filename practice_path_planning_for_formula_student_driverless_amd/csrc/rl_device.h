@@ -13,6 +13,12 @@ namespace rl {
 
 // libstdc++ std::max / std::min / std::clamp comparison forms (NaN behaviour included)
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
+// a wave-uniform double held in an SGPR pair (readfirstlane): fp64 values computed on the
+// VALU land in VGPRs, where a kernel-lifetime constant would occupy two registers per lane
+__device__ __forceinline__ double uni(double x) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(x)));
+}
 __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
 __device__ __forceinline__ double sclamp(double v, double lo, double hi) { return (v < lo) ? lo : ((hi < v) ? hi : v); }
 

@@ -212,6 +212,7 @@ struct alignas(16) Smem {
     double red[3][NW];           // per-wave partial sums of an evaluation
     double red2[2][NW];          // other block reductions
     double bc[4];                // broadcast scalars
+    VConst vc;                   // v-pass constants (read per v pass: no registers held across the kernel)
     union {
         double2 coef[2][K][T];   // [0]: (A1,A2)  [1]: (N0,W)   (precompute_lin_geom_generic)
         double vin[2][T];        // v-pass relaxation: published outgoing values
@@ -310,13 +311,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
     const double Lb = p.Ls ? p.Ls[blockIdx.x] : p.L;
-    const double h = Lb / (double)N;                     // ref:690 / 913
+    // (uni: the kernel-lifetime constants live in SGPR pairs, not in VGPRs)
+    const double h = uni(Lb / (double)N);                // ref:690 / 913
     const double* __restrict__ CEN = p.center + (size_t)blockIdx.x * (size_t)p.center_stride;
-    const double invh = 1.0 / h, inv2h = 1.0 / (2 * h), invh2 = 1.0 / (h * h);   // ref:547, 562
-    const double m2invh2 = -2 * invh2;                   // ref:577 (-2*invh2)
-    const double two_h = 2 * h, hh = h * h;              // ref:602-603 divisors
+    const double invh = uni(1.0 / h), inv2h = uni(1.0 / (2 * h)), invh2 = uni(1.0 / (h * h));   // ref:547, 562
+    const double m2invh2 = uni(-2 * invh2);              // ref:577 (-2*invh2)
+    const double two_h = uni(2 * h), hh = uni(h * h);    // ref:602-603 divisors
     const double lam = C.lambda_smooth;
-    const double lam2 = 2.0 * lam;                       // ref:673 2.0*lambda_smooth*gsm
+    const double lam2 = uni(2.0 * lam);                  // ref:673 2.0*lambda_smooth*gsm
     const double lam_act = active ? lam : 0.0;           // inactive lanes' Σa1² drops out of J
     const bool is_last = tid == Ta - 1;
     const bool wrap_lane = tail_wave && is_last;         // the closed wrap's right neighbour is sample 0
@@ -488,17 +490,21 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     };
 
     // ---- v(s) profile: velocity_profile_forward_backward ref:782-862 ---------
-    VConst vc;
-    vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;   // ref:802-804
-    vc.a_total2 = vc.a_total * vc.a_total;
-    vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;     // ref:810 constant prefix
-    vc.Fr = C.mass_kg * 9.81 * C.c_rr;                   // ref:811
-    vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
-    vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
-    vc.h = h; vc.two_h = 2.0 * h;
+    if (tid == 0) {
+        VConst vc;
+        vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;   // ref:802-804
+        vc.a_total2 = vc.a_total * vc.a_total;
+        vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;     // ref:810 constant prefix
+        vc.Fr = C.mass_kg * 9.81 * C.c_rr;                   // ref:811
+        vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
+        vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
+        vc.h = h; vc.two_h = 2.0 * h;
+        sm.vc = vc;          // first read after the outer loop's first barrier
+    }
 
     // returns sweeps executed; padding samples hold ka=0, v=+inf (never bind)
     auto vpass = [&](const double (&ka)[K], double (&v)[K]) RL_AI -> int {
+        const VConst vc = sm.vc;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double kk = fabs(ka[k]);
@@ -626,7 +632,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // 2.0*(g1+g2) + lam2*gsm. Scaling by 2 is exact, so 2*(g1+g2) = 2*g1 + 2*g2 and
     // 2*g1 = D1T(q1) with the coefficients doubled (likewise D2T(q2)), bit for bit as
     // long as no product is subnormal: the factor 2 costs no multiplication.
-    const double inv2h_x2 = 2.0 * inv2h, invh_x2 = 2.0 * invh, invh2_x2 = 2.0 * invh2, m2invh2_x2 = 2.0 * m2invh2;
+    const double inv2h_x2 = uni(2.0 * inv2h), invh_x2 = uni(2.0 * invh), invh2_x2 = uni(2.0 * invh2),
+                 m2invh2_x2 = uni(2.0 * m2invh2);
     auto d1t_x2 = [&](int k, double vm, double v0, double vp) RL_AI -> double {   // 2*D1T (ref:555-557 / 567-572)
         if (CLOSED) return (vm - vp) * inv2h_x2;
         const int j = base + k;

@@ -124,12 +124,13 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
     const double Lb = p.Ls ? p.Ls[blockIdx.x] : p.L;
-    const double h = Lb / (double)N;                     // ref:690 / 913
+    // (uni: the kernel-lifetime constants live in SGPR pairs, not in VGPRs)
+    const double h = uni(Lb / (double)N);                // ref:690 / 913
     const double* __restrict__ CEN = p.center + (size_t)blockIdx.x * (size_t)p.center_stride;
-    const double invh = 1.0 / h, inv2h = 1.0 / (2 * h), invh2 = 1.0 / (h * h);   // ref:547, 562
-    const double m2invh2 = -2 * invh2;
-    const double two_h = 2 * h, hh = h * h;
-    const double lam = C.lambda_smooth, lam2 = 2.0 * lam;
+    const double invh = uni(1.0 / h), inv2h = uni(1.0 / (2 * h)), invh2 = uni(1.0 / (h * h));   // ref:547, 562
+    const double m2invh2 = uni(-2 * invh2);
+    const double two_h = uni(2 * h), hh = uni(h * h);
+    const double lam = C.lambda_smooth, lam2 = uni(2.0 * lam);
 
     const size_t off = (size_t)b * (size_t)N;
     double* __restrict__ X = p.x + off;
