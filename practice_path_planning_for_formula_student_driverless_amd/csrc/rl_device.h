@@ -13,6 +13,10 @@ namespace rl {
 
 // libstdc++ std::max / std::min / std::clamp comparison forms (NaN behaviour included)
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
+// a - 2*b as the reference evaluates it (two roundings: 2*b, then the difference), in one
+// instruction: 2*b is exact (barring overflow past 8.9e307), so the fused form rounds the
+// same exact value once, zero signs included
+__device__ __forceinline__ double sub2x(double a, double b) { return __builtin_fma(-2.0, b, a); }
 // a wave-uniform double held in an SGPR pair (readfirstlane): fp64 values computed on the
 // VALU land in VGPRs, where a kernel-lifetime constant would occupy two registers per lane
 __device__ __forceinline__ double uni(double x) {
@@ -62,7 +66,7 @@ __device__ __forceinline__ double vstep_fwd(const VConst& c, double vi, double k
     double a_power = (c.Pmax > 0 && vi > 1e-6) ? (c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass) : 1e9;
     double a_acc = smin(smin(a_res, c.acc_cap), a_power);
     a_acc = smax(0.0, a_acc);
-    return sqrt(smax(0.0, vi * vi + 2.0 * a_acc * c.h));
+    return sqrt(smax(0.0, __builtin_fma(2.0, a_acc * c.h, vi * vi)));   // 2*(a*h) is exact: the sum's one rounding
 }
 // backward step (ref:841-845): a_brk = ax_max_at(v,k).second
 __device__ __forceinline__ double vstep_bwd(const VConst& c, double vi, double ki) {
@@ -71,7 +75,7 @@ __device__ __forceinline__ double vstep_bwd(const VConst& c, double vi, double k
     double Fd = c.kFd * vi * vi;
     double a_brk = smin(a_res, c.brk_cap) + (Fd + c.Fr) / c.mass;
     a_brk = smax(0.0, a_brk);
-    return sqrt(smax(0.0, vi * vi + 2.0 * a_brk * c.h));
+    return sqrt(smax(0.0, __builtin_fma(2.0, a_brk * c.h, vi * vi)));
 }
 
 }  // namespace rl

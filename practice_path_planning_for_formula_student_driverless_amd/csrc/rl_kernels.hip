@@ -415,18 +415,18 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         if (N == 1) { xp = 1; yp = 0; xpp = ypp = 0; return; }
         if (CLOSED) {
             xp = (px[k + 3] - px[k + 1]) / two_h; yp = (py[k + 3] - py[k + 1]) / two_h;
-            xpp = (px[k + 3] - 2 * px[k + 2] + px[k + 1]) / hh; ypp = (py[k + 3] - 2 * py[k + 2] + py[k + 1]) / hh;
+            xpp = (sub2x(px[k + 3], px[k + 2]) + px[k + 1]) / hh; ypp = (sub2x(py[k + 3], py[k + 2]) + py[k + 1]) / hh;
         } else if (i == 0) {
             xp = (px[k + 3] - px[k + 2]) / h; yp = (py[k + 3] - py[k + 2]) / h;
-            if (N >= 3) { xpp = (px[k + 4] - 2 * px[k + 3] + px[k + 2]) / hh; ypp = (py[k + 4] - 2 * py[k + 3] + py[k + 2]) / hh; }
+            if (N >= 3) { xpp = (sub2x(px[k + 4], px[k + 3]) + px[k + 2]) / hh; ypp = (sub2x(py[k + 4], py[k + 3]) + py[k + 2]) / hh; }
             else xpp = ypp = 0;
         } else if (i == N - 1) {
             xp = (px[k + 2] - px[k + 1]) / h; yp = (py[k + 2] - py[k + 1]) / h;
-            if (N >= 3) { xpp = (px[k + 2] - 2 * px[k + 1] + px[k]) / hh; ypp = (py[k + 2] - 2 * py[k + 1] + py[k]) / hh; }
+            if (N >= 3) { xpp = (sub2x(px[k + 2], px[k + 1]) + px[k]) / hh; ypp = (sub2x(py[k + 2], py[k + 1]) + py[k]) / hh; }
             else xpp = ypp = 0;
         } else {
             xp = (px[k + 3] - px[k + 1]) / two_h; yp = (py[k + 3] - py[k + 1]) / two_h;
-            xpp = (px[k + 3] - 2 * px[k + 2] + px[k + 1]) / hh; ypp = (py[k + 3] - 2 * py[k + 2] + py[k + 1]) / hh;
+            xpp = (sub2x(px[k + 3], px[k + 2]) + px[k + 1]) / hh; ypp = (sub2x(py[k + 3], py[k + 2]) + py[k + 1]) / hh;
         }
     };
     // normals_from_points_generic ref:581-593, own valid samples -> NX/NY
@@ -611,10 +611,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         return (ap - am) * inv2h;
     };
     auto d2_at = [&](int k, double am, double a0, double ap) RL_AI -> double {   // D2 ref:552-554 / 573-575
-        if (CLOSED) return (ap - 2 * a0 + am) * invh2;
+        if (CLOSED) return (sub2x(ap, a0) + am) * invh2;
         const int i = base + k;
         if (N <= 2 || i == 0 || i == N - 1) return 0.0;
-        return (ap - 2 * a0 + am) * invh2;
+        return (sub2x(ap, a0) + am) * invh2;
     };
     auto d1t_at = [&](int k, double vm, double v0, double vp) RL_AI -> double {  // D1T ref:555-557 / 567-572
         if (CLOSED) return (vm - vp) * inv2h;
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         return acc;
     };
     auto d2t_x2 = [&](int k, double vm, double v0, double vp) RL_AI -> double {   // 2*D2T (ref:558 / 576-578)
-        if (CLOSED) return (vp - 2 * v0 + vm) * invh2_x2;
+        if (CLOSED) return (sub2x(vp, v0) + vm) * invh2_x2;
         const int j = base + k;
         if (N <= 2) return 0.0;
         double acc = 0.0;

@@ -165,18 +165,18 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         if (CLOSED) {
             const int ip = next_i(i), im = prev_i(i);
             xp = (X[ip] - X[im]) / two_h; yp = (Y[ip] - Y[im]) / two_h;
-            xpp = (X[ip] - 2 * X[i] + X[im]) / hh; ypp = (Y[ip] - 2 * Y[i] + Y[im]) / hh;
+            xpp = (sub2x(X[ip], X[i]) + X[im]) / hh; ypp = (sub2x(Y[ip], Y[i]) + Y[im]) / hh;
         } else if (i == 0) {
             xp = (X[1] - X[0]) / h; yp = (Y[1] - Y[0]) / h;
-            if (N >= 3) { xpp = (X[2] - 2 * X[1] + X[0]) / hh; ypp = (Y[2] - 2 * Y[1] + Y[0]) / hh; }
+            if (N >= 3) { xpp = (sub2x(X[2], X[1]) + X[0]) / hh; ypp = (sub2x(Y[2], Y[1]) + Y[0]) / hh; }
             else xpp = ypp = 0;
         } else if (i == N - 1) {
             xp = (X[N - 1] - X[N - 2]) / h; yp = (Y[N - 1] - Y[N - 2]) / h;
-            if (N >= 3) { xpp = (X[N - 1] - 2 * X[N - 2] + X[N - 3]) / hh; ypp = (Y[N - 1] - 2 * Y[N - 2] + Y[N - 3]) / hh; }
+            if (N >= 3) { xpp = (sub2x(X[N - 1], X[N - 2]) + X[N - 3]) / hh; ypp = (sub2x(Y[N - 1], Y[N - 2]) + Y[N - 3]) / hh; }
             else xpp = ypp = 0;
         } else {
             xp = (X[i + 1] - X[i - 1]) / two_h; yp = (Y[i + 1] - Y[i - 1]) / two_h;
-            xpp = (X[i + 1] - 2 * X[i] + X[i - 1]) / hh; ypp = (Y[i + 1] - 2 * Y[i] + Y[i - 1]) / hh;
+            xpp = (sub2x(X[i + 1], X[i]) + X[i - 1]) / hh; ypp = (sub2x(Y[i + 1], Y[i]) + Y[i - 1]) / hh;
         }
     };
     // normals_from_points_generic ref:581-593
@@ -213,9 +213,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         return (ap - am) * inv2h;
     };
     auto d2_at = [&](int i, double am, double a0, double ap) -> double {
-        if (CLOSED) return (ap - 2 * a0 + am) * invh2;
+        if (CLOSED) return (sub2x(ap, a0) + am) * invh2;
         if (N <= 2 || i == 0 || i == N - 1) return 0.0;
-        return (ap - 2 * a0 + am) * invh2;
+        return (sub2x(ap, a0) + am) * invh2;
     };
     auto d1t_at = [&](int j, double vm, double v0, double vp) -> double {
         if (CLOSED) return (vm - vp) * inv2h;
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         return acc;
     };
     auto d2t_at = [&](int j, double vm, double v0, double vp) -> double {
-        if (CLOSED) return (vp - 2 * v0 + vm) * invh2;
+        if (CLOSED) return (sub2x(vp, v0) + vm) * invh2;
         if (N <= 2) return 0.0;
         double acc = 0.0;
         if (j - 1 >= 1 && j - 1 <= N - 2) acc += (+invh2) * vm;
