@@ -58,7 +58,7 @@ struct RingHost {
     std::vector<uint32_t> flag;     // [M/32]
     std::vector<double> blk;        // [M/8][4] block circles (rl_corridor.h block culling)
     int M = 0, E = 0;
-    double dl0 = 0;
+    double dl0 = 0, dl32 = 0;
 };
 
 RingHost make_ring(const double* s, int E) {
@@ -92,7 +92,9 @@ RingHost make_ring(const double* s, int E) {
     // NaN/inf coordinates make dl0 non-finite: every pair is then a candidate and the
     // exact expressions propagate the values like the reference
     R.dl0 = 4e-12 * (1.0 + vmax) + 4e-15 * rv;
-    if (!(vmax == vmax) || !(rv == rv)) R.dl0 = nan;
+    R.dl32 = 1e-6 * rv;
+    if (!(vmax == vmax) || !(rv == rv)) R.dl0 = R.dl32 = nan;
+    if (!(rv <= 1e30)) R.dl32 = INFINITY;          // beyond fp32 range: the fp32 filter keeps every pair
     // Per block of RL_BLK entries: a circle holding both endpoints of every segment that
     // ends in the block (the start point of the segment ending at v is entry v-1's
     // vertex, bit for bit). R = -1: no segment ends there; R = +inf: a non-finite
@@ -123,6 +125,22 @@ RingHost make_ring(const double* s, int E) {
         o[1] = cy;
         o[2] = finite ? rad * (1.0 + 1e-9) + 1e-12 * (1.0 + std::fabs(cx) + std::fabs(cy)) : INFINITY;
     }
+    // fp32 copies for the side filter (rl_corridor.h ring_rays): vertices, then block
+    // circles with the radius rounded up; packed after the fp64 circles
+    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb, 0.0f);
+    for (int v = 0; v < 2 * R.M; ++v) f32[v] = (float)R.vtx[v];
+    for (int b = 0; b < nb; ++b) {
+        float* o = &f32[(size_t)2 * R.M + (size_t)4 * b];
+        o[0] = (float)R.blk[(size_t)4 * b];
+        o[1] = (float)R.blk[(size_t)4 * b + 1];
+        const double rb = R.blk[(size_t)4 * b + 2];
+        float rf = (float)rb;
+        if ((double)rf < rb) rf = std::nextafter(rf, INFINITY);
+        o[2] = rf;
+    }
+    const size_t n64 = R.blk.size();
+    R.blk.resize(rl::ring_blk_doubles((size_t)R.M), 0.0);
+    std::memcpy(&R.blk[n64], f32.data(), f32.size() * sizeof(float));
     return R;
 }
 
@@ -158,7 +176,7 @@ struct rl_plan {
     uint32_t* d_flag = nullptr;
     double* d_blk = nullptr;
     int ring_M[2] = {0, 0};
-    double ring_dl0[2] = {0, 0};
+    double ring_dl0[2] = {0, 0}, ring_dl32[2] = {0, 0};
     rl_cfg* d_cfg = nullptr;
     uint64_t* d_seeds = nullptr;
     ModeBufs mb[2];
@@ -330,12 +348,12 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
     const size_t N = (size_t)std::max(p->N, 1), BN = (size_t)B * N;
     RingHost rh[2] = {make_ring(prob->inner_seg, prob->Ei), make_ring(prob->outer_seg, prob->Eo)};
     const size_t Mt = (size_t)rh[0].M + rh[1].M;
-    for (int r = 0; r < 2; ++r) { p->ring_M[r] = rh[r].M; p->ring_dl0[r] = rh[r].dl0; }
+    for (int r = 0; r < 2; ++r) { p->ring_M[r] = rh[r].M; p->ring_dl0[r] = rh[r].dl0; p->ring_dl32[r] = rh[r].dl32; }
     p->center_stride = centers ? (int64_t)2 * (int64_t)N : 0;
     if (Ls && (rc = p->alloc(&p->d_Ls, (size_t)B))) return cleanup(rc);
     if ((rc = p->alloc(&p->d_center, centers ? 2 * N * (size_t)B : 2 * N)) || (rc = p->alloc(&p->d_vtx, 2 * Mt)) ||
         (rc = p->alloc(&p->d_rec, Mt)) || (rc = p->alloc(&p->d_flag, Mt / 32)) ||
-        (rc = p->alloc(&p->d_blk, 4 * (Mt / rl::RL_BLK))) || (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
+        (rc = p->alloc(&p->d_blk, rl::ring_blk_doubles(Mt))) || (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
         return cleanup(rc);
     hipStream_t st = p->own_stream;
     if (p->N > 0 && hipMemcpyAsync(p->d_center, centers ? centers : prob->center_xy,
@@ -349,7 +367,7 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
         if (hipMemcpyAsync(p->d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(p->d_blk + 4 * (size_t)(off / rl::RL_BLK), R.blk.data(), R.blk.size() * sizeof(double),
+            hipMemcpyAsync(p->d_blk + rl::ring_blk_doubles((size_t)off), R.blk.data(), R.blk.size() * sizeof(double),
                            hipMemcpyHostToDevice, st))
             return cleanup(fail(RL_EHIP, "upload rings"));
         // the copies read the host vectors: wait before they go out of scope
@@ -422,10 +440,11 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
             kp.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
             kp.ring[r].rec = p->d_rec + off;
             kp.ring[r].flag = p->d_flag + off / 32;
-            kp.ring[r].blk = p->d_blk + 4 * (size_t)(off / rl::RL_BLK);
+            kp.ring[r].blk = p->d_blk + rl::ring_blk_doubles((size_t)off);
             kp.ring[r].M = p->ring_M[r];
             kp.ring[r].E = r == 0 ? p->Ei : p->Eo;
             kp.ring[r].dl0 = p->ring_dl0[r];
+            kp.ring[r].dl32 = p->ring_dl32[r];
         }
         kp.cfg = p->d_cfg;
         kp.seeds = p->d_seeds;
@@ -501,7 +520,7 @@ int rl_corridor(const rl_problem* prob, const rl_cfg* cfg, int32_t device, doubl
     double* d_vtx = (double*)dalloc(2 * Mt * sizeof(double));
     rl::SegRec* d_rec = (rl::SegRec*)dalloc(Mt * sizeof(rl::SegRec));
     uint32_t* d_flag = (uint32_t*)dalloc(Mt / 32 * sizeof(uint32_t));
-    double* d_blk = (double*)dalloc(4 * (Mt / rl::RL_BLK) * sizeof(double));
+    double* d_blk = (double*)dalloc(rl::ring_blk_doubles(Mt) * sizeof(double));
     if (!d_c || !d_out || !d_vtx || !d_rec || !d_flag || !d_blk) return release(fail(RL_ENOMEM, "rl_corridor: hipMalloc failed"));
     rl::CorrParams c{};
     c.center = d_c;
@@ -518,15 +537,16 @@ int rl_corridor(const rl_problem* prob, const rl_cfg* cfg, int32_t device, doubl
                  hipMemcpy(d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
                  hipMemcpy(d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice) == hipSuccess &&
                  hipMemcpy(d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess &&
-                 hipMemcpy(d_blk + 4 * (size_t)(off / rl::RL_BLK), R.blk.data(), R.blk.size() * sizeof(double),
+                 hipMemcpy(d_blk + rl::ring_blk_doubles((size_t)off), R.blk.data(), R.blk.size() * sizeof(double),
                            hipMemcpyHostToDevice) == hipSuccess;
         c.ring[r].vtx = (const double2*)(d_vtx + 2 * (size_t)off);
         c.ring[r].rec = d_rec + off;
         c.ring[r].flag = d_flag + off / 32;
-        c.ring[r].blk = d_blk + 4 * (size_t)(off / rl::RL_BLK);
+        c.ring[r].blk = d_blk + rl::ring_blk_doubles((size_t)off);
         c.ring[r].M = R.M;
         c.ring[r].E = R.E;
         c.ring[r].dl0 = R.dl0;
+        c.ring[r].dl32 = R.dl32;
     }
     if (!ok) return release(fail(RL_EHIP, "rl_corridor: upload"));
     if (rl::launch_corridor(c, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -581,7 +601,7 @@ int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double
     double* d_vtx = (double*)dalloc(2 * Mt * sizeof(double));
     rl::SegRec* d_rec = (rl::SegRec*)dalloc(Mt * sizeof(rl::SegRec));
     uint32_t* d_flag = (uint32_t*)dalloc(Mt / 32 * sizeof(uint32_t));
-    double* d_blk = (double*)dalloc(4 * (Mt / rl::RL_BLK) * sizeof(double));
+    double* d_blk = (double*)dalloc(rl::ring_blk_doubles(Mt) * sizeof(double));
     double* d_rows = (double*)dalloc((size_t)nrows * RL_GEOM_COLS * sizeof(double));
     if (!d_kn || !d_vtx || !d_rec || !d_flag || !d_blk || !d_rows) return release(fail(RL_ENOMEM, "rl_geom: hipMalloc failed"));
     hipStream_t st = nullptr;
@@ -604,17 +624,18 @@ int rl_geom(const rl_geom_problem* gp, const rl_cfg* cfg, int32_t device, double
             if (hipMemcpyAsync(d_vtx + 2 * (size_t)off, R.vtx.data(), R.vtx.size() * sizeof(double), hipMemcpyHostToDevice, st) ||
                 hipMemcpyAsync(d_rec + off, R.rec.data(), R.rec.size() * sizeof(rl::SegRec), hipMemcpyHostToDevice, st) ||
                 hipMemcpyAsync(d_flag + off / 32, R.flag.data(), R.flag.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st) ||
-                hipMemcpyAsync(d_blk + 4 * (size_t)(off / rl::RL_BLK), R.blk.data(), R.blk.size() * sizeof(double),
+                hipMemcpyAsync(d_blk + rl::ring_blk_doubles((size_t)off), R.blk.data(), R.blk.size() * sizeof(double),
                                hipMemcpyHostToDevice, st))
                 return finish(fail(RL_EHIP, "rl_geom: upload rings"));
         }
         g.ring[r].vtx = (const double2*)(d_vtx + 2 * (size_t)off);
         g.ring[r].rec = d_rec + off;
         g.ring[r].flag = d_flag + off / 32;
-        g.ring[r].blk = d_blk + 4 * (size_t)(off / rl::RL_BLK);
+        g.ring[r].blk = d_blk + rl::ring_blk_doubles((size_t)off);
         g.ring[r].M = R.M;
         g.ring[r].E = R.E;
         g.ring[r].dl0 = R.dl0;
+        g.ring[r].dl32 = R.dl32;
     }
     g.kx = d_kn;
     g.ky = d_kn + 5 * (size_t)nk;

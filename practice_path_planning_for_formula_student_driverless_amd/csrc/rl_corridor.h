@@ -45,10 +45,15 @@ struct RingDesc {
     const double2* vtx;       // [M] entry vertex (NaN for padding)
     const SegRec* rec;        // [M] record of the segment ending at the entry
     const uint32_t* flag;     // [M/32] bit (31-j): entry 32b+j ends a segment
-    const double* blk;        // [M/8][4] block circles (cx, cy, R, 0); R < 0: no segment ends in the block
+    const double* blk;        // ring_blk_doubles(M): [M/8][4] block circles (cx, cy, R, 0), R < 0: no segment
+                              // ends in the block; then the side filter's fp32 copies: vertices [M][2] f32
+                              // and block circles [M/8][4] f32 (radius rounded up)
     int32_t M, E;             // padded entry count, segment count
     double dl0;               // 4e-12*(1+Vmax) + 4e-15*Rv
+    double dl32;              // 1e-6*Rv: the fp32 side filter's extra margin (see ring_rays)
 };
+__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return M / 2 + M + M / 4; }
+typedef __attribute__((address_space(4))) const float cflt;
 
 // Block culling. Entries come in blocks of 8. The host gives each block a circle (C, R)
 // that contains both endpoints of every segment ending in the block (rl_abi.cpp
@@ -116,20 +121,31 @@ template <int CK>
 __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
                                           const double (&ux)[CK], const double (&uy)[CK], const bool (&act)[CK],
                                           double (&bp)[CK], double (&bn)[CK], double (&ub2)[CK]) {
-    cdbl* V = as_cdbl(R.vtx);              // [M][2]
     cu32* F = as_cu32(R.flag);
-    cdbl* BK = as_cdbl(R.blk);             // [M/8][4]
+    cflt* V = (cflt*)(R.blk + R.M / 2);                  // fp32 vertices [M][2]
+    cflt* BK = (cflt*)(R.blk + R.M / 2 + R.M);           // fp32 block circles [M/8][4]
     const SegRec* __restrict__ S = R.rec;  // per-lane (divergent) reads
-    double dl[CK], g[CK];
+    // The side filter runs in fp32 (packed for two samples per lane).  c = n x (V - P) =
+    // ux*vy - uy*vx - g.  With e = 2^-24 and |n| <= 1, the fp32 value built from fp32
+    // copies of n, V, g differs from the exact one by <= 5e(|vx|+|vy|+|g|) <= 3e-7(Rv+|q|_1),
+    // and the fp64 value (the one the skip proof above bounds by dl) by <= dl/6; so with
+    // dl32 = dl + 1e-6(Rv+|q|_1), c32 > dl32 implies c64 > dl: a pair the fp32 filter skips
+    // is one the fp64 filter would skip.  Block test: the fp32 centre is within e|C|_1 of
+    // the exact one and R is rounded up, so |c32(C)| > R(1+1e-6) + 2 dl32 leaves every
+    // endpoint with |c32| > 2 dl32 - 11e(Rv+|q|_1) >= dl32 on the centre's side.
+    float dl[CK], g[CK], uxf[CK], uyf[CK];
     uint64_t pp[CK], pn[CK];       // side masks of the previous entry (wave lane masks, SGPR)
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
-        // c = n x (V - P) = ux*vy - uy*vx - g: |c_f - c| <= 6e-16 (Rv + |qx| + |qy|)
-        g[k] = ux[k] * qy[k] - uy[k] * qx[k];
-        dl[k] = R.dl0 + 4e-15 * (fabs(qx[k]) + fabs(qy[k]));
+        const double q1 = fabs(qx[k]) + fabs(qy[k]);
+        g[k] = (float)(ux[k] * qy[k] - uy[k] * qx[k]);
+        dl[k] = (float)((R.dl0 + 4e-15 * q1) + (R.dl32 + 1e-6 * q1));
+        uxf[k] = (float)ux[k];
+        uyf[k] = (float)uy[k];
         bp[k] = bn[k] = ub2[k] = INFINITY;
         pp[k] = pn[k] = 0ull;
     }
+    auto side = [&](int k, float vx, float vy) -> float { return __builtin_fmaf(uxf[k], vy, -__builtin_fmaf(uyf[k], vx, g[k])); };
     bool prev_ok = false;          // pp/pn hold the sides of the entry just before the next one
     for (int b0 = 0; b0 < R.M; b0 += 32) {
         uint32_t w[CK];
@@ -139,14 +155,14 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
         uint32_t visit = 0u;
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
-            cdbl* bk = BK + 4 * ((b0 / RL_BLK) + q);
-            const double cx = bk[0], cy = bk[1], rb = bk[2];
+            cflt* bk = BK + 4 * ((b0 / RL_BLK) + q);
+            const float cx = bk[0], cy = bk[1], rb = bk[2];
             bool need = false;
-            if (rb >= 0.0) {
+            if (rb >= 0.0f) {
 #pragma unroll
                 for (int k = 0; k < CK; ++k) {
-                    const double c = __builtin_fma(ux[k], cy, -__builtin_fma(uy[k], cx, g[k]));
-                    need |= act[k] && !(fabs(c) > rb * (1.0 + 1e-9) + 2.0 * dl[k]);
+                    const float c = side(k, cx, cy);
+                    need |= act[k] && !(fabsf(c) > rb * (1.0f + 1e-6f) + 2.0f * dl[k]);
                 }
             }
             if (__any(need)) visit |= 1u << q;
@@ -163,20 +179,20 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
             }
             const int e0 = b0 + q * RL_BLK;
             if (!prev_ok && e0 > 0) {      // sides of the entry before the block
-                const double vx = V[2 * (e0 - 1)], vy = V[2 * (e0 - 1) + 1];
+                const float vx = V[2 * (e0 - 1)], vy = V[2 * (e0 - 1) + 1];
 #pragma unroll
                 for (int k = 0; k < CK; ++k) {
-                    const double c = __builtin_fma(ux[k], vy, -__builtin_fma(uy[k], vx, g[k]));
+                    const float c = side(k, vx, vy);
                     pp[k] = __builtin_amdgcn_ballot_w64(c > dl[k]);
                     pn[k] = __builtin_amdgcn_ballot_w64(c < -dl[k]);
                 }
             }
 #pragma unroll
             for (int j = 0; j < RL_BLK; ++j) {
-                const double vx = V[2 * (e0 + j)], vy = V[2 * (e0 + j) + 1];
+                const float vx = V[2 * (e0 + j)], vy = V[2 * (e0 + j) + 1];
 #pragma unroll
                 for (int k = 0; k < CK; ++k) {
-                    const double c = __builtin_fma(ux[k], vy, -__builtin_fma(uy[k], vx, g[k]));
+                    const float c = side(k, vx, vy);
                     const uint64_t P = __builtin_amdgcn_ballot_w64(c > dl[k]);
                     const uint64_t Q = __builtin_amdgcn_ballot_w64(c < -dl[k]);
                     const uint64_t cand = ~((P & pp[k]) | (Q & pn[k]));
