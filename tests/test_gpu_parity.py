@@ -556,6 +556,22 @@ def _corridor_cases():
         inner_seg=raceline.ring_edges(np.stack([27 * np.cos(k) + 3 * np.cos(3 * k), 15.5 * np.sin(k)], axis=1)),
         outer_seg=raceline.ring_edges(np.stack([33 * np.cos(k) + 3 * np.cos(3 * k), 20.5 * np.sin(k)], axis=1)),
         veh_width=1.0, closed=True)))
+    # rays through ring vertices, 4e4 m from the origin: every third sample's ±n ray
+    # passes (up to one rounding) through a vertex of each ring, so side values sit at
+    # ~1e-12 of the line while fp32 copies of the coordinates err by ~1e-3 m -- the fp32
+    # side filter's margin has to keep these pairs (rl_corridor.h ring_rays)
+    N = 600
+    t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+    center = np.stack([4e4 + 25 * np.cos(t) + 2 * np.cos(2 * t), -3e4 + 16 * np.sin(t)], axis=1)
+    tx = (np.roll(center[:, 0], -1) - np.roll(center[:, 0], 1)) * 0.5
+    ty = (np.roll(center[:, 1], -1) - np.roll(center[:, 1], 1)) * 0.5
+    nn = np.sqrt(tx * tx + ty * ty)
+    nx, ny = -ty / nn, tx / nn
+    sel = np.arange(0, N, 3)
+    inner = np.stack([center[sel, 0] - 2.1 * nx[sel], center[sel, 1] - 2.1 * ny[sel]], axis=1)
+    outer = np.stack([center[sel, 0] + 1.7 * nx[sel], center[sel, 1] + 1.7 * ny[sel]], axis=1)
+    out.append(("vertex_rays_far", abi.Problem(center=center, L=1.0, inner_seg=raceline.ring_edges(inner),
+                                               outer_seg=raceline.ring_edges(outer), veh_width=0.6, closed=True)))
     return out
 
 
