@@ -127,7 +127,7 @@ RingHost make_ring(const double* s, int E) {
     }
     // fp32 copies for the side filter (rl_corridor.h ring_rays): vertices, then block
     // circles with the radius rounded up; packed after the fp64 circles
-    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb, 0.0f);
+    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M, 0.0f);
     for (int v = 0; v < 2 * R.M; ++v) f32[v] = (float)R.vtx[v];
     for (int b = 0; b < nb; ++b) {
         float* o = &f32[(size_t)2 * R.M + (size_t)4 * b];
@@ -137,6 +137,15 @@ RingHost make_ring(const double* s, int E) {
         float rf = (float)rb;
         if ((double)rf < rb) rf = std::nextafter(rf, INFINITY);
         o[2] = rf;
+    }
+    for (int v = 0; v < R.M; ++v) {     // segment midpoints and half lengths (rounded up)
+        float* o = &f32[(size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * v];
+        o[0] = (float)R.rec[v].mx;
+        o[1] = (float)R.rec[v].my;
+        const double hr = R.rec[v].hr;
+        float hf = (float)hr;
+        if ((double)hf < hr) hf = std::nextafter(hf, INFINITY);
+        o[2] = hf;
     }
     const size_t n64 = R.blk.size();
     R.blk.resize(rl::ring_blk_doubles((size_t)R.M), 0.0);

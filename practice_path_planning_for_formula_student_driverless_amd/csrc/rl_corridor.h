@@ -47,12 +47,13 @@ struct RingDesc {
     const uint32_t* flag;     // [M/32] bit (31-j): entry 32b+j ends a segment
     const double* blk;        // ring_blk_doubles(M): [M/8][4] block circles (cx, cy, R, 0), R < 0: no segment
                               // ends in the block; then the side filter's fp32 copies: vertices [M][2] f32
-                              // and block circles [M/8][4] f32 (radius rounded up)
+                              // and block circles [M/8][4] f32 (radius rounded up), and the fallback
+                              // filters' segment midpoints [M][4] f32 (mx, my, half length rounded up, 0)
     int32_t M, E;             // padded entry count, segment count
     double dl0;               // 4e-12*(1+Vmax) + 4e-15*Rv
     double dl32;              // 1e-6*Rv: the fp32 side filter's extra margin (see ring_rays)
 };
-__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return M / 2 + M + M / 4; }
+__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return M / 2 + M + M / 4 + 2 * M; }
 typedef __attribute__((address_space(4))) const float cflt;
 
 // Block culling. Entries come in blocks of 8. The host gives each block a circle (C, R)
@@ -246,9 +247,9 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
 template <int CK, bool TIGHT = true, bool PRUNE = true>
 __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
                                              const bool (&need)[CK], const double (&rad)[CK], double (&md)[CK]) {
-    cdbl* SR = as_cdbl(R.rec);             // [M][8] SegRec fields (uniform reads)
     cu32* F = as_cu32(R.flag);
-    cdbl* BK = as_cdbl(R.blk);
+    cflt* BK = (cflt*)(R.blk + R.M / 2 + R.M);            // fp32 block circles [M/8][4]
+    cflt* MD = (cflt*)(R.blk + R.M / 2 + R.M + R.M / 4);   // fp32 (mx, my, hr, 0) [M][4]
     const SegRec* __restrict__ S = R.rec;
     const double cx = qx[0], cy = qy[0];
     double dk[CK];                         // |q_k - q0|_1, rounded up
@@ -261,21 +262,34 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
         if (need[k]) Rl = fmax(Rl, rad[k] + dk[k]);
         lneed |= need[k];
     }
+    // The block and midpoint filters run in fp32 on fp32 copies (circle radii and half
+    // lengths rounded up).  |q0 - C| computed so differs from the exact distance by at most
+    // 2e(|q0|_1 + Rv) + 3e|q0 - C| (e = 2^-24, |C|_1 <= Rv for circle centres and
+    // midpoints); dm = dl32 + 1e-6|q0|_1 >= 1e-6(Rv + |q0|_1) covers the first term, the
+    // (1 + 1e-6) factors the second: a skip in fp32 is a skip in exact arithmetic, and the
+    // nearest-midpoint distance + dm bounds the exact one from above.
+    const float cxf = (float)cx, cyf = (float)cy;
+    const float dm = (float)(R.dl32 + 1e-6 * (fabs(cx) + fabs(cy)));
+    auto d2f = [&](float px, float py) -> float {
+        const float dx = cxf - px, dy = cyf - py;
+        return __builtin_fmaf(dx, dx, dy * dy);
+    };
+    float Rlf = (float)(Rl * (1.0 + 1e-6));
     // blocks whose circle meets the search circle (wave-uniform mask of one word)
     auto visit_of = [&](int b0) -> uint32_t {
         uint32_t visit = 0u;
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
-            cdbl* bk = BK + 4 * ((b0 / RL_BLK) + q);
-            const double dx = cx - bk[0], dy = cy - bk[1], rb = bk[2];
-            const double r = (Rl + rb) * (1.0 + 1e-12);
-            const bool nb = lneed && rb >= 0.0 && !(dx * dx + dy * dy > r * r);
+            cflt* bk = BK + 4 * ((b0 / RL_BLK) + q);
+            const float rb = bk[2];
+            const float r = (Rlf + rb + dm) * (1.0f + 1e-6f);
+            const bool nb = lneed && rb >= 0.0f && !(d2f(bk[0], bk[1]) > r * r);
             if (__any(nb)) visit |= 1u << q;
         }
         return visit;
     };
     // pass 1: nearest midpoint (padding and chain starts carry NaN mids: fmin skips them)
-    double m2 = INFINITY;
+    float m2 = INFINITY;
     for (int b0 = 0; TIGHT && b0 < R.M; b0 += 32) {
         const uint32_t visit = visit_of(b0);
         if (visit == 0u) continue;
@@ -284,19 +298,19 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
             if (!((visit >> q) & 1u)) continue;
 #pragma unroll
             for (int j = 0; j < RL_BLK; ++j) {
-                cdbl* sr = SR + 8 * (b0 + q * RL_BLK + j);
-                const double dx = cx - sr[5], dy = cy - sr[6];
-                m2 = fmin(m2, dx * dx + dy * dy);
+                cflt* mr = MD + 4 * (b0 + q * RL_BLK + j);
+                m2 = fminf(m2, d2f(mr[0], mr[1]));
             }
         }
     }
     if (isfinite(m2)) {
-        const double m = sqrt(m2) * (1.0 + 1e-12) + 1e-12;
+        const double m = (double)(sqrtf(m2) * (1.0f + 1e-6f) + dm) * (1.0 + 1e-12) + 1e-12;
         double R2 = -1.0;
 #pragma unroll
         for (int k = 0; k < CK; ++k)
             if (need[k]) R2 = fmax(R2, fmin(rad[k], m + dk[k]) + dk[k]);
         Rl = R2;
+        Rlf = (float)(Rl * (1.0 + 1e-6));
     }
     // pass 2: candidates and the exact distances
     for (int b0 = 0; b0 < R.M; b0 += 32) {
@@ -309,10 +323,9 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
             if (!((visit >> q) & 1u)) { w <<= RL_BLK; continue; }
 #pragma unroll
             for (int j = 0; j < RL_BLK; ++j) {
-                cdbl* sr = SR + 8 * (b0 + q * RL_BLK + j);
-                const double mx = sr[5], my = sr[6], hr = sr[7];
-                const double dx = cx - mx, dy = cy - my, r = Rl + hr;
-                const bool skip = dx * dx + dy * dy > r * r;
+                cflt* mr = MD + 4 * (b0 + q * RL_BLK + j);
+                const float r = (Rlf + mr[2] + dm) * (1.0f + 1e-6f);
+                const bool skip = d2f(mr[0], mr[1]) > r * r;
                 w = (w << 1) | (uint32_t)!skip;
             }
         }

@@ -311,7 +311,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
     const double Lb = p.Ls ? p.Ls[blockIdx.x] : p.L;
-    // (uni: the kernel-lifetime constants live in SGPR pairs, not in VGPRs)
+    // (uni: the kernel-lifetime constants live in SGPR pairs, not in VGPRs.  Besides the
+    // registers this saves, it keeps them out of the register allocator's VGPR/AGPR
+    // live-range copies: with this compiler such a copy can be placed inside a divergent
+    // region (the ragged init loop below), so the lanes outside EXEC kept a stale copy --
+    // seen as ax = 0/(garbage 2h) = -0 on the last, partial chunk of an open track; an SGPR
+    // copy is lane-independent)
     const double h = uni(Lb / (double)N);                // ref:690 / 913
     const double* __restrict__ CEN = p.center + (size_t)blockIdx.x * (size_t)p.center_stride;
     const double invh = uni(1.0 / h), inv2h = uni(1.0 / (2 * h)), invh2 = uni(1.0 / (h * h));   // ref:547, 562
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         vc.Fr = C.mass_kg * 9.81 * C.c_rr;                   // ref:811
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
         vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
-        vc.h = h; vc.two_h = 2.0 * h;
+        vc.h = h; vc.two_h = two_h;          // two_h = uni(2*h): the same value, from an SGPR pair
         sm.vc = vc;          // first read after the outer loop's first barrier
     }
 
@@ -857,7 +862,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                             if (i + 1 < N) v1 = (k + 1 < cnt) ? v[(k + 1 < K) ? k + 1 : k] : rv;
                             else v1 = CLOSED ? rv : v[k];
                             double v0 = v[k];
-                            p.ax[off + i] = (v1 * v1 - v0 * v0) / (2.0 * h);
+                            p.ax[off + i] = (v1 * v1 - v0 * v0) / two_h;   // ref:857 (2.0*h)
                             p.v[off + i] = v0;
                             lt += h / smax(1e-6, v[k]);
                         }

@@ -245,7 +245,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     vc.Fr = C.mass_kg * 9.81 * C.c_rr;
     vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
     vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
-    vc.h = h; vc.two_h = 2.0 * h;
+    vc.h = h; vc.two_h = two_h;          // two_h = uni(2*h): the same value, from an SGPR pair
     const int Cr = (N + TS - 1) / TS;
     const int r0 = min(N, tid * Cr), r1 = min(N, r0 + Cr);
     const bool ract = r0 < r1;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 for (int i = tid; i < N; i += TS) {                // ref:854-860
                     const int j = (i + 1 < N) ? i + 1 : (CLOSED ? 0 : i);
                     const double v0 = V[i], v1 = V[j];
-                    p.ax[off + i] = (v1 * v1 - v0 * v0) / (2.0 * h);
+                    p.ax[off + i] = (v1 * v1 - v0 * v0) / two_h;   // ref:857 (2.0*h)
                     p.v[off + i] = v0;
                     lt[0] += h / smax(1e-6, v0);
                 }

@@ -43,7 +43,8 @@ def zero_signs_equal(got, ref, what):
     ref = np.asarray(ref)
     z = ref == 0.0
     bad = np.flatnonzero(z & (np.signbit(got) != np.signbit(ref)))
-    assert bad.size == 0, f"{what}: {bad.size} zeros with the wrong sign (first at {bad[:5]})"
+    assert bad.size == 0, (f"{what}: {bad.size} zeros with the wrong sign (first at {bad[:5]}: "
+                           f"got {got.ravel()[bad[:3]].tolist()} ref {ref.ravel()[bad[:3]].tolist()})")
 
 
 def compare_outputs(got: abi.Outputs, ref: abi.Outputs, mintime: bool, label: str, counters=True):
