@@ -135,7 +135,6 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
     // the exact one and R is rounded up, so |c32(C)| > R(1+1e-6) + 2 dl32 leaves every
     // endpoint with |c32| > 2 dl32 - 11e(Rv+|q|_1) >= dl32 on the centre's side.
     float dl[CK], g[CK], uxf[CK], uyf[CK];
-    uint64_t pp[CK], pn[CK];       // side masks of the previous entry (wave lane masks, SGPR)
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
         const double q1 = fabs(qx[k]) + fabs(qy[k]);
@@ -144,10 +143,23 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
         uxf[k] = (float)ux[k];
         uyf[k] = (float)uy[k];
         bp[k] = bn[k] = ub2[k] = INFINITY;
-        pp[k] = pn[k] = 0ull;
     }
     auto side = [&](int k, float vx, float vy) -> float { return __builtin_fmaf(uxf[k], vy, -__builtin_fmaf(uyf[k], vx, g[k])); };
-    bool prev_ok = false;          // pp/pn hold the sides of the entry just before the next one
+    // Side bits without mask logic: c > dl <=> sign(dl - c) and c < -dl <=> sign(c + dl), exact
+    // for finite operands (a rounded difference keeps the sign of the exact one, equality gives
+    // +0); v_alignbit shifts each sign bit straight into a per-lane word.  A lane whose sample or
+    // margin is not finite takes every pair as a candidate (as the compare form did with NaN).
+    // NaN sides only come from the padding entries at the end of the stream, whose bits the
+    // segment flags mask.
+    bool bad[CK];
+    uint32_t lp[CK], lq[CK];       // side bits of the entry just before the next block
+#pragma unroll
+    for (int k = 0; k < CK; ++k) {
+        bad[k] = !(isfinite(g[k]) && isfinite(dl[k]) && isfinite(uxf[k]) && isfinite(uyf[k]));
+        lp[k] = lq[k] = 0u;
+    }
+    auto sgn = [](float x) -> uint32_t { return __float_as_uint(x) >> 31; };
+    bool prev_ok = false;          // lp/lq hold the sides of the entry just before the next block
     for (int b0 = 0; b0 < R.M; b0 += 32) {
         uint32_t w[CK];
 #pragma unroll
@@ -179,13 +191,21 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
                 continue;
             }
             const int e0 = b0 + q * RL_BLK;
-            if (!prev_ok && e0 > 0) {      // sides of the entry before the block
-                const float vx = V[2 * (e0 - 1)], vy = V[2 * (e0 - 1) + 1];
+            uint32_t pb[CK], qb[CK];   // bit 8: the entry before the block, bit 7-j: entry e0+j
 #pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    const float c = side(k, vx, vy);
-                    pp[k] = __builtin_amdgcn_ballot_w64(c > dl[k]);
-                    pn[k] = __builtin_amdgcn_ballot_w64(c < -dl[k]);
+            for (int k = 0; k < CK; ++k) { pb[k] = lp[k]; qb[k] = lq[k]; }
+            if (!prev_ok) {
+                if (e0 > 0) {          // sides of the entry before the block
+                    const float vx = V[2 * (e0 - 1)], vy = V[2 * (e0 - 1) + 1];
+#pragma unroll
+                    for (int k = 0; k < CK; ++k) {
+                        const float c = side(k, vx, vy);
+                        pb[k] = sgn(dl[k] - c);
+                        qb[k] = sgn(c + dl[k]);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CK; ++k) pb[k] = qb[k] = 0u;
                 }
             }
 #pragma unroll
@@ -194,13 +214,18 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
 #pragma unroll
                 for (int k = 0; k < CK; ++k) {
                     const float c = side(k, vx, vy);
-                    const uint64_t P = __builtin_amdgcn_ballot_w64(c > dl[k]);
-                    const uint64_t Q = __builtin_amdgcn_ballot_w64(c < -dl[k]);
-                    const uint64_t cand = ~((P & pp[k]) | (Q & pn[k]));
-                    w[k] = (w[k] << 1) | (uint32_t)__builtin_amdgcn_inverse_ballot_w64(cand);
-                    pp[k] = P;
-                    pn[k] = Q;
+                    pb[k] = __builtin_amdgcn_alignbit(pb[k], __float_as_uint(dl[k] - c), 31);
+                    qb[k] = __builtin_amdgcn_alignbit(qb[k], __float_as_uint(c + dl[k]), 31);
                 }
+            }
+#pragma unroll
+            for (int k = 0; k < CK; ++k) {
+                // a pair is skipped only when both endpoints lie beyond dl on the same side
+                uint32_t cand = ~((pb[k] & (pb[k] >> 1)) | (qb[k] & (qb[k] >> 1))) & 0xFFu;
+                if (bad[k]) cand = 0xFFu;
+                w[k] = (w[k] << RL_BLK) | cand;
+                lp[k] = pb[k] & 1u;
+                lq[k] = qb[k] & 1u;
             }
             prev_ok = true;
         }
