@@ -63,6 +63,11 @@ __device__ unsigned long long rl_dbg_stamps[16384][8];
 #define RL_STAMP(slot) do {} while (0)
 #endif
 
+// std::pow for a non-default time_gamma_power (ref:960), out of line: inlined, its
+// temporaries competed with the kernel's live state for registers (min-time (8,256):
+// 328 -> 192 B/lane scratch); the default power 2 never calls it
+__device__ __attribute__((noinline)) double pow_noinline(double x, double y) { return pow(x, y); }
+
 // ------------------------------------------------------------ wave primitives
 // x from another lane for patterns where every lane has a source (quad_perm, row_ror):
 // no `old` operand, so no register has to be zeroed first
@@ -899,7 +904,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     r = smin(1.0, smax(0.0, r));
                     double rp;
                     if (C.time_gamma_power == 2.0) rp = r * r;           // GCC folds pow(r, 2.0) to r*r
-                    else { rp = pow(r, C.time_gamma_power); __builtin_amdgcn_sched_barrier(0); }
+                    else rp = pow_noinline(r, C.time_gamma_power);
                     double corner_w = 1.0 + C.w_time_gain * rp;
                     double invv_w = 1.0;
                     if (C.time_weight_use_inv_v) {
