@@ -22,9 +22,10 @@ for B in (256, 4096):
     for r in range(4):
         for n, (lib, h) in plans.items():
             assert lib.rl_plan_run(h, None) == 0
-            m1, m2 = C.c_float(), C.c_float()
+            m0, m1, m2 = C.c_float(), C.c_float(), C.c_float()
+            lib.rl_plan_kernel_ms(h, 0, C.byref(m0))
             lib.rl_plan_kernel_ms(h, 1, C.byref(m1)); lib.rl_plan_kernel_ms(h, 2, C.byref(m2))
-            res[n].append((m1.value, m2.value))
+            res[n].append((m1.value, m2.value, m0.value))
     outs = {}
     for n, (lib, h) in plans.items():
         o1 = abi.Outputs.alloc(B, prob.N, 14, False); o2 = abi.Outputs.alloc(B, prob.N, 14, True)
@@ -37,7 +38,7 @@ for B in (256, 4096):
         a = np.array(res[n][1:])
         same = all(np.array_equal(getattr(outs[n], f), getattr(outs[base], f))
                    for f in ("x", "y", "alpha_last", "v", "ax", "lap"))
-        print(f"C3 B={B:5d} {n:8s} min-curv {np.median(a[:, 0]):7.2f} ms  min-time {np.median(a[:, 1]):7.2f} ms  "
+        print(f"C3 B={B:5d} {n:8s} min-curv {np.median(a[:, 0]):7.2f} ms  min-time {np.median(a[:, 1]):7.2f} ms  run {np.median(a[:, 2]):7.2f} ms  "
               f"bitexact_vs_{base}: {same}", flush=True)
         if not same:
             print("    differs:", [f for f in ("x", "y", "alpha_last", "v", "ax", "lap", "evals", "accepts")
