@@ -238,7 +238,48 @@ def cpu_leg(budget_s: float) -> dict:
     res["c3_oracle_laps"] = {"seeds": c3_seeds, "laps": unchunk(r3, workers, len(jobs))}
     res["c4_oracle_laps"] = unchunk(r4, workers, len(c4_jobs))
     res["oracle_pool"] = {"workers": workers, "seconds": round(time.perf_counter() - t0, 1)}
+    # ---- open-mode line: the first seeds through the oracle
+    oprob, ocfg = open_problem()
+    omc, omt = O.run_oracle(oprob, ocfg, seeds=list(range(OPEN_CHECK)), B=OPEN_CHECK)
+    res["open_oracle"] = {"x": omc.x.tolist(), "evals": omc.evals.tolist(), "lap": omt.lap.tolist(),
+                          "mt_evals": omt.evals.tolist()}
     return res
+
+
+def open_problem():
+    """C2's track as an open path (is_closed_track = false: DiffOpsOpen ref:560-579, open
+    normals/heading ref:581-620): the open-mode throughput line."""
+    case, prob, cfg = load_problem("cmap1_n2000")
+    return abi.Problem(center=prob.center, L=prob.L, inner_seg=raceline.edges_for(case["inner_ring"], False),
+                       outer_seg=raceline.edges_for(case["outer_ring"], False),
+                       veh_width=prob.veh_width, closed=False), cfg
+
+
+def run_open(local, B: int = 1024):
+    """Open-mode throughput: C2's problem with closed = false, B seeds, both optimisers."""
+    prob, cfg = open_problem()
+    MO = int(cfg.max_outer_iters)
+    plan = raceline.Plan(prob, cfg, seeds=np.arange(B, dtype=np.uint64), B=B,
+                         modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, device=local)
+    plan.run()
+    ms = {1: [], 2: []}
+    for _ in range(3):
+        plan.run()
+        for i in (1, 2):
+            ms[i].append(plan.kernel_ms(i))
+    mc, mt = plan.fetch()
+    plan.close()
+    k1, k2 = float(np.median(ms[1])), float(np.median(ms[2]))
+    res = {"N": prob.N, "instances": B, "kernel_ms_mincurv": round(k1, 3), "kernel_ms_mintime": round(k2, 3),
+           "outer_iters_per_s_mincurv": round(B * MO / (k1 * 1e-3), 1),
+           "outer_iters_per_s_mintime": round(B * MO / (k2 * 1e-3), 1),
+           "kernels": "rl_optimize_kernel<8,256,open,mincurv> / <8,256,open,mintime>"}
+    gpu = {"x": mc.x[:OPEN_CHECK].tolist(), "evals": mc.evals[:OPEN_CHECK].tolist(),
+           "lap": mt.lap[:OPEN_CHECK].tolist(), "mt_evals": mt.evals[:OPEN_CHECK].tolist()}
+    return res, gpu
+
+
+OPEN_CHECK = 8     # seeds of the open-mode line checked against the oracle (CPU leg)
 
 
 def start_cpu_leg(budget_s: float):
@@ -603,6 +644,7 @@ def main():
             extras["c5_oval_n10000"] = c5
             extras["c2_pcie_inclusive"] = run_c2_pcie(prob, cfg, B, MO, rank)
             extras["dropin_b1_latency"] = run_dropin(local)
+            extras["open_mode_n2000"], open_gpu = run_open(local)
             extras["step6_geom_cmap1_n2000"] = run_step6(world, rank)
             xh, yh = res["x"].cpu().numpy(), res["y"].cpu().numpy()
             extras["lap_eval_1024_racelines_n2000"] = run_lapeval(world, rank, np.stack([xh, yh], axis=2))
@@ -691,6 +733,14 @@ def main():
                 if r:
                     v["reference_cpu_mincurv_ms"] = r["mincurv_ms"]
                     v["reference_cpu_mintime_ms"] = r["mintime_ms"]
+        if "open_mode_n2000" in extras and cpu_res.get("open_oracle"):
+            oo = cpu_res["open_oracle"]
+            gx, ox = np.array(open_gpu["x"]), np.array(oo["x"])
+            extras["open_mode_n2000"]["vs_oracle"] = {
+                "seeds": list(range(OPEN_CHECK)),
+                "x_max_abs": float(np.max(np.abs(gx - ox))), "x_tol": 1e-4 * float(np.max(np.abs(ox))) + 1e-9,
+                "lap_max_rel": float(np.max(np.abs(np.array(open_gpu["lap"]) - np.array(oo["lap"])) / np.abs(oo["lap"]))),
+                "evals_equal": open_gpu["evals"] == oo["evals"] and open_gpu["mt_evals"] == oo["mt_evals"]}
         extras["cpu_oracle_pool"] = cpu_res.get("oracle_pool")
 
     out = {
