@@ -22,12 +22,8 @@ VARIANTS = {
     "sck4": {"RL_SCK": 4},
     "sts512": {"RL_STS": 512},
     "sts256": {"RL_STS": 256},
-    "xbar": {"RL_XBAR": 1},
     "ck4tight": {"RL_CK": 4, "RL_MD_TIGHT": 1},
     "ck1": {"RL_CK": 1},
-    "stag150": {"RL_STAGGER": 150},
-    "stag300": {"RL_STAGGER": 300},
-    "stag600": {"RL_STAGGER": 600},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }
