@@ -675,9 +675,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 
     // ---- state ------------------------------------------------------------
     double G2[K];                                   // γ² (min-time)
-    // corridor, α and α_trial, the gradient at α; (al, gr) and (an, gn) swap roles on
-    // every accepted step (PGD loop), so nothing is copied
-    double lo[K], hi[K], al[K], gr[K], an[K], gn[K];
+    // corridor, α and α_trial, the gradient at α; al and an swap roles on every accepted
+    // step (PGD loop), so nothing is copied.  One gradient array: an accepted trial's
+    // gradient overwrites the old one, which nothing reads after the trial's evaluation
+    double lo[K], hi[K], al[K], gr[K], an[K];
     double q1[K], q2[K], a1v[K];                    // gradient stencil inputs of the last evaluation
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
@@ -973,20 +974,21 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         eval_grad(gr);
         int evals = 1, accepts = 0, it = 0;
         double J_prev = J;
-        // One inner iteration (ref:726-742) from (cur, gc): trials in nxt, the gradient of
-        // an accepted trial into gx.  Returns 2: accepted, go on (nxt is current); 1: stop
-        // with nxt current; 0: stop with cur current.  The loop below alternates the
-        // roles of (al, gr) and (an, gn), so an accepted step copies nothing.
-        auto inner = [&](const double (&cur)[K], const double (&gc)[K], double (&nxt)[K], double (&gx)[K]) RL_AI -> int {
+        // One inner iteration (ref:726-742) from (cur, g): trials in nxt; an accepted trial's
+        // gradient replaces g (the projection and the Armijo decrease have read g by then;
+        // a rejected trial leaves it).  Returns 2: accepted, go on (nxt is current); 1: stop
+        // with nxt current; 0: stop with cur current.  The loop below alternates the roles
+        // of al and an, so an accepted step copies nothing.
+        auto inner = [&](const double (&cur)[K], double (&g)[K], double (&nxt)[K]) RL_AI -> int {
             if (it >= max_inner) return 0;
             ++it;
             int bt = 0;
             for (;;) {
-                project(cur, gc, nxt);
-                double Jn = eval_j(nxt, cur, gc, true, dec);
+                project(cur, g, nxt);
+                double Jn = eval_j(nxt, cur, g, true, dec);
                 ++evals;
                 if (Jn <= J + armijo_c * dec) {
-                    eval_grad(gx);
+                    eval_grad(g);
                     J = Jn;
                     ++accepts;
                     break;
@@ -1001,9 +1003,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         };
         bool in_an = false;
         for (;;) {
-            int r = inner(al, gr, an, gn);
+            int r = inner(al, gr, an);
             if (r != 2) { in_an = (r == 1); break; }
-            r = inner(an, gn, al, gr);
+            r = inner(an, gr, al);
             if (r != 2) { in_an = (r == 0); break; }
         }
         if (in_an) {
