@@ -680,6 +680,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // gradient overwrites the old one, which nothing reads after the trial's evaluation
     double lo[K], hi[K], al[K], gr[K], an[K];
     double q1[K], q2[K], a1v[K];                    // gradient stencil inputs of the last evaluation
+    // Min-curv keeps A1, A2, N0 of its own samples in registers from lin-geom on (the single
+    // gradient array left the room: 247 VGPRs, no scratch) and reads only W from LDS per
+    // evaluation.  A/B (build knob RL_A12_REG = 0 / 1 / 2: none / A1,A2 / A1,A2,N0 in
+    // registers): C2 8.81 / 8.71 / 8.69 ms, bit-exact.  Min-time has no room (γ²).
+#ifndef RL_A12_REG
+#define RL_A12_REG 2
+#endif
+    constexpr bool A12R = RL_A12_REG && !MT;        // (A1, A2) in registers instead of LDS
+    constexpr bool N0R = RL_A12_REG >= 2 && !MT;    // and N0
+    double A1r[K], A2r[K], N0r[K];
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
     // of the trial vector a: J (uniform across the workgroup) and the Armijo
@@ -710,8 +720,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         double jr[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const double2 c01 = sm.u.coef[0][k][tid];   // (A1, A2)
-            const double2 c23 = sm.u.coef[1][k][tid];   // (N0, W)
+            const double2 c01 = A12R ? make_double2(A1r[k], A2r[k]) : sm.u.coef[0][k][tid];   // (A1, A2)
+            const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
             double am = (k > 0) ? a[k - 1] : lv;
             double ap = (k + 1 < K) ? a[k + 1] : rv;
             double x1 = d1_at(k, am, a[k], ap);
@@ -939,7 +949,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 double denom = pow15(smax(1e-12, xp * xp + yp * yp));
                 double w = 1.0 / denom;
                 const bool v = k < cnt;
-                sm.u.coef[0][k][tid] = make_double2(v ? a1 : 0.0, v ? a2 : 0.0);
+                if (A12R) { A1r[k] = v ? a1 : 0.0; A2r[k] = v ? a2 : 0.0; }
+                if (N0R) N0r[k] = v ? n0 : 0.0;
+                else sm.u.coef[0][k][tid] = make_double2(v ? a1 : 0.0, v ? a2 : 0.0);
                 sm.u.coef[1][k][tid] = make_double2(v ? n0 : 0.0, v ? w : 0.0);
             }
         }

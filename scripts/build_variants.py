@@ -24,6 +24,9 @@ VARIANTS = {
     "sts256": {"RL_STS": 256},
     "ck4tight": {"RL_CK": 4, "RL_MD_TIGHT": 1},
     "ck1": {"RL_CK": 1},
+    "a12_0": {"RL_A12_REG": 0},
+    "a12_1": {"RL_A12_REG": 1},
+    "a12_2": {"RL_A12_REG": 2},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }
