@@ -683,12 +683,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // Min-curv keeps A1, A2, N0 of its own samples in registers from lin-geom on (the single
     // gradient array left the room: 247 VGPRs, no scratch) and reads only W from LDS per
     // evaluation.  A/B (build knob RL_A12_REG = 0 / 1 / 2: none / A1,A2 / A1,A2,N0 in
-    // registers): C2 8.81 / 8.71 / 8.69 ms, bit-exact.  Min-time has no room (γ²).
+    // registers): C2 8.81 / 8.71 / 8.69 ms, bit-exact.  Min-time has no room (γ²), nor has
+    // the open K = 8 min-curv kernel (its boundary stencils: scratch 100 -> 172 B/lane, the
+    // open C2-shaped run 21.4 -> 25.0 ms).
 #ifndef RL_A12_REG
 #define RL_A12_REG 2
 #endif
-    constexpr bool A12R = RL_A12_REG && !MT;        // (A1, A2) in registers instead of LDS
-    constexpr bool N0R = RL_A12_REG >= 2 && !MT;    // and N0
+    constexpr bool A12R = RL_A12_REG && !MT && (CLOSED || K < 8);   // (A1, A2) in registers instead of LDS
+    constexpr bool N0R = A12R && RL_A12_REG >= 2;                    // and N0
     double A1r[K], A2r[K], N0r[K];
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
