@@ -512,6 +512,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         sm.vc = vc;          // first read after the outer loop's first barrier
     }
 
+    auto same_bits = [](double a, double b) RL_AI -> bool { return __double_as_longlong(a) == __double_as_longlong(b); };
     // returns sweeps executed; padding samples hold ka=0, v=+inf (never bind)
     auto vpass = [&](const double (&ka)[K], double (&v)[K]) RL_AI -> int {
         const VConst vc = sm.vc;
@@ -531,26 +532,44 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #pragma unroll
             for (int k = 0; k < K; ++k) vstart[k] = v[k];
             // ---- forward pass (ref:829-833)
+            // A chunk re-evaluated with a new incoming value stops as soon as a value equals,
+            // bit for bit, the one it already holds from its previous evaluation in this pass:
+            // the rest of the chunk and its outgoing value would repeat (each step depends only
+            // on the previous value).  The wave stops when all its lanes have.  The relaxation
+            // ends when no published value changed.
             {
                 double in_prev = -1.0;       // sentinel (valid values are >= 0 or +inf)
+                double out = 0.0;            // the value this chunk publishes
                 for (int it = 0;; ++it) {
                     double in = INFINITY;    // first iteration: no incoming constraint
                     if (it > 0 && has_left) in = sm.u.vin[(it - 1) & 1][tid - 1];
                     bool changed = false;
                     if (active && in != in_prev) {
-                        changed = (it > 0);
                         in_prev = in;
                         double cur = vstart[0];
                         if (has_left) cur = smin(vstart[0], in);     // v[i+1] = min(v[i+1], vf)
+                        bool go = (it == 0) || !same_bits(cur, v[0]);
                         v[0] = cur;
 #pragma unroll
                         for (int k = 0; k + 1 < K; ++k) {
-                            double vf = vstep_fwd(vc, v[k], ka[k]);
-                            v[k + 1] = (k + 1 < cnt) ? smin(vstart[k + 1], vf) : INFINITY;
+                            if (!__any(go)) break;
+                            if (go) {
+                                const double vf = vstep_fwd(vc, v[k], ka[k]);
+                                const double nv = (k + 1 < cnt) ? smin(vstart[k + 1], vf) : INFINITY;
+                                go = (it == 0) || !same_bits(nv, v[k + 1]);
+                                v[k + 1] = nv;
+                            }
                         }
-                        if (has_right) sm.u.vin[it & 1][tid] = vstep_fwd(vc, v[K - 1], ka[K - 1]);
+                        if (has_right) {
+                            if (go) {
+                                const double o = vstep_fwd(vc, v[K - 1], ka[K - 1]);
+                                changed = (it > 0) && (o != out);
+                                out = o;
+                            }
+                            sm.u.vin[it & 1][tid] = out;
+                        }
                     } else if (active && has_right) {
-                        sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
+                        sm.u.vin[it & 1][tid] = out;
                     }
                     if (!__syncthreads_or(changed) && it > 0) break;
                 }
@@ -566,29 +585,43 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 if (tid == 0) v[0] = smin(v[0], sm.bc[0]);
                 __syncthreads();
             }
-            // ---- backward pass (ref:841-845)
+            // ---- backward pass (ref:841-845), with the same early stop
             {
                 double vpre[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) vpre[k] = v[k];
                 double in_prev = -1.0;
+                double out = 0.0;
                 for (int it = 0;; ++it) {
                     double in = INFINITY;
                     if (it > 0 && has_right) in = sm.u.vin[(it - 1) & 1][tid + 1];
                     bool changed = false;
                     if (active && in != in_prev) {
-                        changed = (it > 0);
                         in_prev = in;
                         // has_right => full chunk (only the last thread can be partial)
-                        v[K - 1] = has_right ? smin(vpre[K - 1], in) : vpre[K - 1];
+                        const double cur = has_right ? smin(vpre[K - 1], in) : vpre[K - 1];
+                        bool go = (it == 0) || !same_bits(cur, v[K - 1]);
+                        v[K - 1] = cur;
 #pragma unroll
                         for (int k = K - 2; k >= 0; --k) {
-                            double vb = vstep_bwd(vc, v[k + 1], ka[k + 1]);
-                            v[k] = (k < cnt) ? smin(vpre[k], vb) : INFINITY;
+                            if (!__any(go)) break;
+                            if (go) {
+                                const double vb = vstep_bwd(vc, v[k + 1], ka[k + 1]);
+                                const double nv = (k < cnt) ? smin(vpre[k], vb) : INFINITY;
+                                go = (it == 0) || !same_bits(nv, v[k]);
+                                v[k] = nv;
+                            }
                         }
-                        if (has_left) sm.u.vin[it & 1][tid] = vstep_bwd(vc, v[0], ka[0]);
+                        if (has_left) {
+                            if (go) {
+                                const double o = vstep_bwd(vc, v[0], ka[0]);
+                                changed = (it > 0) && (o != out);
+                                out = o;
+                            }
+                            sm.u.vin[it & 1][tid] = out;
+                        }
                     } else if (active && has_left) {
-                        sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
+                        sm.u.vin[it & 1][tid] = out;
                     }
                     if (!__syncthreads_or(changed) && it > 0) break;
                 }
