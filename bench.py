@@ -435,18 +435,31 @@ def run_dropin(local):
     """The reference's own use: one instance per call (pipeline::compute_raceline_and_save
     ref:1347 and compute_mintime_and_save ref:1397), host buffers in and out (PCIe
     included), for the 7 bundled tracks and competition_map1 at N=2000."""
+    import ctypes as C
+
+    lib = abi.load_library()
     out = {}
     for name in DROPIN_CASES:
         case, prob, cfg = load_problem(name)
         raceline.optimize_batch(prob, cfg, None, 1)            # warm-up (module load, first launch)
         t = {"mincurv": [], "mintime": []}
+        k = {"mincurv": [], "mintime": []}
         for _ in range(5):
             for mode in ("mincurv", "mintime"):
                 t0 = time.perf_counter()
                 raceline.optimize_batch(prob, cfg, None, 1, mincurv=mode == "mincurv", mintime=mode == "mintime")
                 t[mode].append(1e3 * (time.perf_counter() - t0))
-        out[name] = {"N": prob.N, "mincurv_ms": round(float(np.median(t["mincurv"])), 3),
-                     "mintime_ms": round(float(np.median(t["mintime"])), 3)}
+                km, cm = C.c_float(), C.c_float()
+                lib.rl_last_call_ms(C.byref(km), C.byref(cm))
+                k[mode].append((km.value, cm.value))
+        med = lambda v: round(float(np.median(v)), 3)   # noqa: E731
+        out[name] = {"N": prob.N, "mincurv_ms": med(t["mincurv"]), "mintime_ms": med(t["mintime"])}
+        for mode in ("mincurv", "mintime"):
+            out[name][mode + "_kernel_ms"] = med([a for a, _ in k[mode]])
+            # inside the C call, outside the kernels: uploads, launch, downloads, host copies
+            out[name][mode + "_abi_overhead_ms"] = med([c - a for a, c in k[mode]])
+            # the Python wrapper's own share (numpy output allocation, ctypes marshalling)
+            out[name][mode + "_python_ms"] = med([w - c for w, (_, c) in zip(t[mode], k[mode])])
     return out
 
 

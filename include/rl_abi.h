@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 3
+#define RL_ABI_VERSION 4
 
 /* error codes */
 #define RL_OK          0
@@ -153,18 +153,30 @@ double rl_seed_value(uint64_t seed, int32_t i, double sigma);
  * Optimise B instances of one problem.  cfg has n_cfg entries (1 = broadcast,
  * or B = one per instance).  seeds has B entries or is NULL (all zero = exactly
  * the reference).  out_mincurv / out_mintime may be NULL to skip that mode.
- * Synchronous: host buffers in, host buffers out (PCIe included).               */
+ * Synchronous: host buffers in, host buffers out (PCIe included), on the calling
+ * thread's current HIP device.  Device plans and pinned staging buffers are reused
+ * across calls from a small process-wide cache keyed by (device, N, B, n_cfg,
+ * max_outer_iters, closed, kernel variant) and the ring segments (bitwise): a repeat
+ * call uploads only the centreline, cfg and seeds.  rl_lap_eval shares the cache.  */
 int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
                 const uint64_t* seeds, int32_t B,
                 rl_out* out_mincurv, rl_out* out_mintime);
+/* Timing of this thread's last successful rl_optimize / rl_lap_eval: *kernel_ms = HIP-event
+ * time from the first to the last kernel of the call, *call_ms = wall time of the whole
+ * call (uploads, kernels, downloads into the caller's buffers).  Either may be NULL.    */
+int rl_last_call_ms(float* kernel_ms, float* call_ms);
+/* Free the idle plans and pinned buffers of the cache (device memory returns to HIP). */
+int rl_release_plan_cache(void);
 
 /* ------------------------------------------------------------ multi-device
  * rl_optimize over n_dev devices (SURVEY.md §8b device list, §8e): the B instances are
  * split into contiguous blocks (block d = instances [B*d/n, B*(d+1)/n), n = min(n_dev, B)),
  * one plan and HIP stream per device, all devices enqueued before the first download;
  * each block's results are copied to its offset of the caller's host outputs (the final
- * gather).  devices: n_dev distinct device indices, or NULL for 0..n_dev-1.  Same
- * cfg/seeds/out conventions and results as rl_optimize (instances are independent). */
+ * gather).  devices: n_dev device indices (a device may repeat: two plans on one device),
+ * or NULL for 0..n_dev-1.  Same cfg/seeds/out conventions and results as rl_optimize
+ * (instances are independent); every cfg is checked before any device work.  The
+ * calling thread's current device is unchanged on return. */
 int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
                       const uint64_t* seeds, int32_t B, const int32_t* devices, int32_t n_dev,
                       rl_out* out_mincurv, rl_out* out_mintime);

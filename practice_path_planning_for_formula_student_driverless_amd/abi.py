@@ -379,6 +379,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                           C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(RlOut),
                                           C.POINTER(RlOut)]
         lib.rl_optimize_multi.restype = C.c_int
+    if hasattr(lib, "rl_last_call_ms"):     # absent only in older experiment builds (A/B bases)
+        lib.rl_last_call_ms.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        lib.rl_last_call_ms.restype = C.c_int
+        lib.rl_release_plan_cache.argtypes = []
+        lib.rl_release_plan_cache.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib
     return lib

@@ -9,7 +9,11 @@
 #include <cstring>
 #include <limits>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rl_abi.h"
@@ -76,8 +80,10 @@ RingHost make_ring(const double* s, int E) {
         ends.push_back(end);
     };
     double vmax = 0, rv = 0;
+    bool nonfinite = false;        // std::max below drops a NaN second argument: tracked here
     for (int e = 0; e < E; ++e) {
         const double* q = s + 4 * e;
+        for (int j = 0; j < 4; ++j) nonfinite |= !std::isfinite(q[j]);
         if (e == 0 || !(q[0] == s[4 * e - 2] && q[1] == s[4 * e - 1])) push(q[0], q[1], dummy, false);
         const rl::SegRec r = make_segrec(q);
         push(q[2], q[3], r, true);
@@ -89,11 +95,12 @@ RingHost make_ring(const double* s, int E) {
     R.flag.assign(R.M / 32, 0u);
     for (int v = 0; v < R.M; ++v)
         if (ends[v]) R.flag[v / 32] |= 0x80000000u >> (v % 32);
-    // NaN/inf coordinates make dl0 non-finite: every pair is then a candidate and the
-    // exact expressions propagate the values like the reference
+    // A NaN/inf coordinate anywhere makes dl0/dl32 NaN: every pair of the ring is then a
+    // candidate (rl_corridor.h `bad`) and the exact expressions propagate the values like
+    // the reference
     R.dl0 = 4e-12 * (1.0 + vmax) + 4e-15 * rv;
     R.dl32 = 1e-6 * rv;
-    if (!(vmax == vmax) || !(rv == rv)) R.dl0 = R.dl32 = nan;
+    if (nonfinite || !(vmax == vmax) || !(rv == rv)) R.dl0 = R.dl32 = nan;
     if (!(rv <= 1e30)) R.dl32 = INFINITY;          // beyond fp32 range: the fp32 filter keeps every pair
     // Per block of RL_BLK entries: a circle holding both endpoints of every segment that
     // ends in the block (the start point of the segment ending at v is entry v-1's
@@ -172,6 +179,7 @@ bool use_stream(int N) {
 struct rl_plan {
     int device = 0;
     int N = 0, B = 0, modes = 0, ncfg = 0, max_outer = 0, closed = 1, Ei = 0, Eo = 0;
+    bool stream = false;              // streaming kernel (use_stream at creation)
     double L = 0, veh_width = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t last_stream = nullptr;
@@ -197,9 +205,16 @@ struct rl_plan {
         hipError_t e = hipMalloc((void**)p, n * sizeof(T));
         if (e != hipSuccess) return fail(RL_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
         allocs.push_back((void*)*p);
+        dev_bytes += n * sizeof(T);
         return RL_OK;
     }
+    size_t dev_bytes = 0;             // device memory held (plan cache budget)
 };
+
+namespace {
+int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
+               int32_t modes, const double* centers, const double* Ls, rl_out* out_mc, rl_out* out_mt, float* kms);
+}  // namespace
 
 extern "C" {
 
@@ -307,10 +322,11 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
     return plan_create_ex(out, device, prob, cfg, n_cfg, seeds, B, modes, nullptr, nullptr);
 }
 
-static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
-                          const uint64_t* seeds, int32_t B, int32_t modes, const double* centers, const double* Ls) {
-    if (!out) return fail(RL_EINVAL, "plan out pointer is NULL");
-    *out = nullptr;
+static int alloc_mode(rl_plan* p, int m);
+
+// argument checks shared by every entry point that builds or reuses a plan (no device call)
+static int check_inputs(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, int32_t B, int32_t modes,
+                        const double* centers) {
     if (!prob || !cfg) return fail(RL_EINVAL, "problem/cfg is NULL");
     if (B < 1) return fail(RL_EINVAL, "B must be >= 1");
     if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
@@ -327,6 +343,15 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
             return fail(RL_EINVAL, "negative iteration count");
     }
     if (prob->N > rl::RL_STREAM_MAX_N) return fail(RL_ETOOBIG, "N exceeds the streaming kernel (N <= 1048576)");
+    return RL_OK;
+}
+
+static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
+                          const uint64_t* seeds, int32_t B, int32_t modes, const double* centers, const double* Ls) {
+    if (!out) return fail(RL_EINVAL, "plan out pointer is NULL");
+    *out = nullptr;
+    if (int rc0 = check_inputs(prob, cfg, n_cfg, B, modes, centers)) return rc0;
+    const int mo = cfg[0].max_outer_iters;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
     if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
@@ -344,6 +369,7 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
     p->veh_width = prob->veh_width;
     p->Ei = prob->Ei;
     p->Eo = prob->Eo;
+    p->stream = use_stream(p->N);
     int rc = RL_OK;
     auto cleanup = [&](int code) {
         rl_plan_destroy(p);
@@ -354,7 +380,7 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
     for (auto& e : p->ev)
         if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
 
-    const size_t N = (size_t)std::max(p->N, 1), BN = (size_t)B * N;
+    const size_t N = (size_t)std::max(p->N, 1);
     RingHost rh[2] = {make_ring(prob->inner_seg, prob->Ei), make_ring(prob->outer_seg, prob->Eo)};
     const size_t Mt = (size_t)rh[0].M + rh[1].M;
     for (int r = 0; r < 2; ++r) { p->ring_M[r] = rh[r].M; p->ring_dl0[r] = rh[r].dl0; p->ring_dl32[r] = rh[r].dl32; }
@@ -388,30 +414,38 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
     if (seeds) std::memcpy(sd.data(), seeds, (size_t)B * sizeof(uint64_t));
     if (hipMemcpyAsync(p->d_seeds, sd.data(), (size_t)B * sizeof(uint64_t), hipMemcpyHostToDevice, st))
         return cleanup(fail(RL_EHIP, "upload seeds"));
-    for (int m = 0; m < 2; ++m) {
-        if (!(modes & (1 << m))) continue;
-        ModeBufs& mb = p->mb[m];
-        if ((rc = p->alloc(&mb.x, BN)) || (rc = p->alloc(&mb.y, BN)) || (rc = p->alloc(&mb.heading, BN)) ||
-            (rc = p->alloc(&mb.kappa, BN)) || (rc = p->alloc(&mb.alpha_total, BN)) ||
-            (rc = p->alloc(&mb.alpha_last, BN)) || (rc = p->alloc(&mb.nx, BN)) || (rc = p->alloc(&mb.ny, BN)) ||
-            (rc = p->alloc(&mb.evals, (size_t)B * std::max(mo, 1))) ||
-            (rc = p->alloc(&mb.accepts, (size_t)B * std::max(mo, 1))))
-            return cleanup(rc);
-        if (m == 1) {
-            if ((rc = p->alloc(&mb.v, BN)) || (rc = p->alloc(&mb.ax, BN)) || (rc = p->alloc(&mb.lap, (size_t)B)) ||
-                (rc = p->alloc(&mb.sweeps, (size_t)B * (mo + 1))))
-                return cleanup(rc);
-        }
-        if (use_stream(p->N)) {
-            double** arrs[rl::RL_STREAM_ARRAYS] = {&mb.sb.al, &mb.sb.an, &mb.sb.gr, &mb.sb.lo, &mb.sb.hi,
-                                                  &mb.sb.a1, &mb.sb.a2, &mb.sb.n0, &mb.sb.w, &mb.sb.q1,
-                                                  &mb.sb.q2, &mb.sb.d1, &mb.sb.g2, &mb.sb.v, &mb.sb.vs};
-            for (auto a : arrs)
-                if ((rc = p->alloc(a, BN))) return cleanup(rc);
-        }
-    }
+    for (int m = 0; m < 2; ++m)
+        if ((modes & (1 << m)) && (rc = alloc_mode(p, m))) return cleanup(rc);
     if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(RL_EHIP, "upload sync"));
     *out = p;
+    return RL_OK;
+}
+
+// result and scratch buffers of mode m (0: min-curv, 1: min-time); a no-op if present
+static int alloc_mode(rl_plan* p, int m) {
+    ModeBufs& mb = p->mb[m];
+    if (mb.nx) return RL_OK;
+    const size_t BN = (size_t)p->B * (size_t)std::max(p->N, 1);
+    const int mo = p->max_outer, B = p->B;
+    int rc;
+    if ((rc = p->alloc(&mb.x, BN)) || (rc = p->alloc(&mb.y, BN)) || (rc = p->alloc(&mb.heading, BN)) ||
+        (rc = p->alloc(&mb.kappa, BN)) || (rc = p->alloc(&mb.alpha_total, BN)) ||
+        (rc = p->alloc(&mb.alpha_last, BN)) || (rc = p->alloc(&mb.nx, BN)) || (rc = p->alloc(&mb.ny, BN)) ||
+        (rc = p->alloc(&mb.evals, (size_t)B * std::max(mo, 1))) ||
+        (rc = p->alloc(&mb.accepts, (size_t)B * std::max(mo, 1))))
+        return rc;
+    if (m == 1) {
+        if ((rc = p->alloc(&mb.v, BN)) || (rc = p->alloc(&mb.ax, BN)) || (rc = p->alloc(&mb.lap, (size_t)B)) ||
+            (rc = p->alloc(&mb.sweeps, (size_t)B * (mo + 1))))
+            return rc;
+    }
+    if (p->stream) {
+        double** arrs[rl::RL_STREAM_ARRAYS] = {&mb.sb.al, &mb.sb.an, &mb.sb.gr, &mb.sb.lo, &mb.sb.hi,
+                                              &mb.sb.a1, &mb.sb.a2, &mb.sb.n0, &mb.sb.w, &mb.sb.q1,
+                                              &mb.sb.q2, &mb.sb.d1, &mb.sb.g2, &mb.sb.v, &mb.sb.vs};
+        for (auto a : arrs)
+            if ((rc = p->alloc(a, BN))) return rc;
+    }
     return RL_OK;
 }
 
@@ -464,7 +498,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
         kp.L = p->L; kp.veh_width = p->veh_width;
         HIPCHK(hipEventRecord(p->ev[1 + m], st));
-        hipError_t e = use_stream(p->N) ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
+        hipError_t e = p->stream ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
     }
     HIPCHK(hipEventRecord(p->ev[3], st));
@@ -486,17 +520,16 @@ int rl_lap_eval(const double* paths_xy, const double* L, int32_t N, int32_t B, i
     pr.N = N;
     pr.closed = closed;
     pr.L = L[0];
-    rl_plan* p = nullptr;
-    int rc = plan_create_ex(&p, device, &pr, c.data(), n_cfg, nullptr, B, RL_MODE_MINTIME, paths_xy, L);
-    if (rc != RL_OK) return rc;
-    if ((rc = rl_plan_run(p, nullptr)) != RL_OK || (rc = rl_plan_fetch(p, nullptr, out)) != RL_OK ||
-        (kernel_ms && (rc = rl_plan_kernel_ms(p, 2, kernel_ms)) != RL_OK)) {
-        std::string e = g_err;
-        rl_plan_destroy(p);
-        g_err = e;
-        return rc;
-    }
-    return rl_plan_destroy(p);
+    int ndev = 0, cur = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RL_ENODEV, "device index out of range");
+    const bool restore = hipGetDevice(&cur) == hipSuccess;
+    HIPCHK(hipSetDevice(device));
+    float ms[3];
+    const int rc = run_cached(&pr, c.data(), n_cfg, nullptr, B, RL_MODE_MINTIME, paths_xy, L, nullptr, out, ms);
+    if (rc == RL_OK && kernel_ms) *kernel_ms = ms[2];
+    if (restore) hipSetDevice(cur);
+    return rc;
 }
 
 // pipeline::compute_geom_and_save rows (ref:1295-1335) on the device
@@ -733,26 +766,41 @@ int rl_plan_kernel_ms(rl_plan* p, int32_t idx, float* ms) {
     return RL_OK;
 }
 
-static int fetch_mode(rl_plan* p, int m, rl_out* o, hipStream_t st) {
-    if (!o) return RL_OK;
-    ModeBufs& mb = p->mb[m];
+// the (host destination, device source, bytes) copies that fill `o` from mode m's results
+struct CopyJob {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+static void out_jobs(const rl_plan* p, int m, const rl_out* o, std::vector<CopyJob>& jobs) {
+    if (!o) return;
+    const ModeBufs& mb = p->mb[m];
     const size_t BN = (size_t)p->B * (size_t)p->N;
-    auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
-        if (!dst || !src || bytes == 0) return RL_OK;
-        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
-        return e == hipSuccess ? RL_OK : fail(RL_EHIP, std::string("download: ") + hipGetErrorString(e));
+    auto add = [&](void* dst, const void* src, size_t bytes) {
+        if (dst && src && bytes) jobs.push_back({dst, src, bytes});
     };
-    int rc;
-    if ((rc = cp(o->x, mb.x, BN * 8)) || (rc = cp(o->y, mb.y, BN * 8)) || (rc = cp(o->heading, mb.heading, BN * 8)) ||
-        (rc = cp(o->kappa, mb.kappa, BN * 8)) || (rc = cp(o->alpha_total, mb.alpha_total, BN * 8)) ||
-        (rc = cp(o->alpha_last, mb.alpha_last, BN * 8)) ||
-        (rc = cp(o->evals, mb.evals, (size_t)p->B * p->max_outer * 4)) ||
-        (rc = cp(o->accepts, mb.accepts, (size_t)p->B * p->max_outer * 4)))
-        return rc;
+    add(o->x, mb.x, BN * 8);
+    add(o->y, mb.y, BN * 8);
+    add(o->heading, mb.heading, BN * 8);
+    add(o->kappa, mb.kappa, BN * 8);
+    add(o->alpha_total, mb.alpha_total, BN * 8);
+    add(o->alpha_last, mb.alpha_last, BN * 8);
+    add(o->evals, mb.evals, (size_t)p->B * p->max_outer * 4);
+    add(o->accepts, mb.accepts, (size_t)p->B * p->max_outer * 4);
     if (m == 1) {
-        if ((rc = cp(o->v, mb.v, BN * 8)) || (rc = cp(o->ax, mb.ax, BN * 8)) || (rc = cp(o->lap, mb.lap, (size_t)p->B * 8)) ||
-            (rc = cp(o->vpass_sweeps, mb.sweeps, (size_t)p->B * (p->max_outer + 1) * 4)))
-            return rc;
+        add(o->v, mb.v, BN * 8);
+        add(o->ax, mb.ax, BN * 8);
+        add(o->lap, mb.lap, (size_t)p->B * 8);
+        add(o->vpass_sweeps, mb.sweeps, (size_t)p->B * (p->max_outer + 1) * 4);
+    }
+}
+
+static int fetch_mode(rl_plan* p, int m, rl_out* o, hipStream_t st) {
+    std::vector<CopyJob> jobs;
+    out_jobs(p, m, o, jobs);
+    for (const CopyJob& j : jobs) {
+        hipError_t e = hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return fail(RL_EHIP, std::string("download: ") + hipGetErrorString(e));
     }
     return RL_OK;
 }
@@ -804,19 +852,295 @@ int rl_plan_device_outputs(rl_plan* p, int32_t which, rl_out* d) {
     return RL_OK;
 }
 
+// ------------------------------------------------------------------ plan cache
+// rl_optimize and rl_lap_eval are the reference's own use: one synchronous call per track
+// and mode (ref:1347, 1397, 1466-1478), host buffers in and out.  Building a plan per call
+// (a hipMalloc per array, a stream, events) and copying through pageable memory cost more
+// than the kernel at small B, so these calls reuse plans from a small process-wide cache,
+// keyed by the plan's shape and the ring segments (compared bit for bit): a hit uploads
+// only the centreline, cfg and seeds.  Every copy is staged through pinned host memory
+// owned by the entry; results are downloaded array by array, each with an event, and
+// host threads copy an array out as soon as its event completes.  An entry in use is
+// checked out, so concurrent callers never share one.  The cache object is never
+// destroyed (no HIP call at process exit); rl_release_plan_cache() frees the idle plans.
+}  // extern "C"
+
+namespace {
+
+constexpr int kCacheEntries = 8;                       // idle plans kept
+constexpr size_t kCacheBytes = (size_t)8 << 30;        // device bytes kept idle
+constexpr int kJobEvents = 32;
+
+struct CacheEntry {
+    rl_plan* p = nullptr;
+    int device = 0, N = 0, B = 0, ncfg = 0, mo = 0, closed = 0, Ei = 0, Eo = 0;
+    bool stream = false, centers = false, Ls = false;
+    std::vector<double> segs;                          // inner then outer segments
+    unsigned char* pin = nullptr;                      // pinned staging
+    size_t pin_bytes = 0;
+    hipEvent_t ev[kJobEvents] = {};
+    uint64_t tick = 0;
+
+    bool same(const CacheEntry& k) const {
+        return device == k.device && N == k.N && B == k.B && ncfg == k.ncfg && mo == k.mo && closed == k.closed &&
+               Ei == k.Ei && Eo == k.Eo && stream == k.stream && centers == k.centers && Ls == k.Ls &&
+               segs.size() == k.segs.size() &&
+               (segs.empty() || std::memcmp(segs.data(), k.segs.data(), segs.size() * sizeof(double)) == 0);
+    }
+    size_t bytes() const { return p ? p->dev_bytes : 0; }
+};
+
+void destroy_entry(CacheEntry* e) {
+    if (!e) return;
+    if (e->p) {
+        hipSetDevice(e->p->device);
+        rl_plan_destroy(e->p);
+    }
+    for (hipEvent_t& v : e->ev)
+        if (v) hipEventDestroy(v);
+    if (e->pin) hipHostFree(e->pin);
+    delete e;
+}
+
+struct PlanCache {
+    std::mutex mu;
+    std::vector<CacheEntry*> idle;
+    uint64_t tick = 0;
+
+    CacheEntry* take(const CacheEntry& key) {
+        std::lock_guard<std::mutex> g(mu);
+        for (size_t i = 0; i < idle.size(); ++i)
+            if (idle[i]->same(key)) {
+                CacheEntry* e = idle[i];
+                idle.erase(idle.begin() + (long)i);
+                return e;
+            }
+        return nullptr;
+    }
+    void give(CacheEntry* e) {
+        std::vector<CacheEntry*> evict;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            e->tick = ++tick;
+            idle.push_back(e);
+            auto total = [&]() {
+                size_t t = 0;
+                for (CacheEntry* q : idle) t += q->bytes();
+                return t;
+            };
+            while (idle.size() > 1 && ((int)idle.size() > kCacheEntries || total() > kCacheBytes)) {
+                auto lru = std::min_element(idle.begin(), idle.end(),
+                                            [](CacheEntry* x, CacheEntry* y) { return x->tick < y->tick; });
+                evict.push_back(*lru);
+                idle.erase(lru);
+            }
+        }
+        for (CacheEntry* q : evict) destroy_entry(q);
+    }
+    void clear() {
+        std::vector<CacheEntry*> all;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            all.swap(idle);
+        }
+        for (CacheEntry* q : all) destroy_entry(q);
+    }
+};
+PlanCache& plan_cache() {
+    static PlanCache* c = new PlanCache();
+    return *c;
+}
+
+thread_local float g_last_kernel_ms = -1.0f, g_last_call_ms = -1.0f;
+
+int ensure_pinned(CacheEntry* e, size_t bytes) {
+    if (bytes <= e->pin_bytes) return RL_OK;
+    if (e->pin) hipHostFree(e->pin);
+    e->pin = nullptr;
+    e->pin_bytes = 0;
+    const size_t want = std::max(bytes, (size_t)1 << 16);
+    if (hipHostMalloc((void**)&e->pin, want, hipHostMallocDefault) != hipSuccess) {
+        e->pin = nullptr;
+        return fail(RL_ENOMEM, "hipHostMalloc (pinned staging) failed");
+    }
+    e->pin_bytes = want;
+    return RL_OK;
+}
+
+// Download `jobs` through the entry's pinned staging (from byte `base` on): one async copy
+// per job on stream st with an event after each (the last event covers any jobs beyond
+// the pool), then host threads copy each job out in 4 MiB pieces as soon as its event has
+// completed, so the host copies overlap the transfers still in flight.
+int download_staged(CacheEntry* e, hipStream_t st, const std::vector<CopyJob>& jobs, size_t base) {
+    struct Piece {
+        unsigned char* dst;
+        const unsigned char* src;
+        size_t bytes;
+        int ev;
+    };
+    std::vector<Piece> pieces;
+    size_t off = base, total = 0;
+    const size_t kPiece = (size_t)4 << 20;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        if (hipMemcpyAsync(e->pin + off, jobs[j].src, jobs[j].bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return fail(RL_EHIP, "download (staged) failed");
+        const int evi = (int)std::min(j, (size_t)kJobEvents - 1);
+        const bool last = j + 1 == jobs.size();
+        if ((size_t)evi == j || last)
+            if (hipEventRecord(e->ev[evi], st) != hipSuccess) return fail(RL_EHIP, "hipEventRecord failed");
+        for (size_t q = 0; q < jobs[j].bytes; q += kPiece)
+            pieces.push_back({(unsigned char*)jobs[j].dst + q, e->pin + off + q, std::min(kPiece, jobs[j].bytes - q), evi});
+        off += (jobs[j].bytes + 255) & ~(size_t)255;
+        total += jobs[j].bytes;
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+            if (hipEventSynchronize(e->ev[pieces[i].ev]) != hipSuccess) {
+                bad = true;
+                return;
+            }
+            std::memcpy(pieces[i].dst, pieces[i].src, pieces[i].bytes);
+        }
+    };
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nthr = total < ((size_t)8 << 20) ? 1 : (int)std::min<size_t>({8, hw, pieces.size()});
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (bad) return fail(RL_EHIP, "download (staged): event wait failed");
+    return RL_OK;
+}
+
+// bytes of the staging area a job list needs (256-B aligned pieces)
+size_t staged_bytes(const std::vector<CopyJob>& jobs) {
+    size_t t = 0;
+    for (const CopyJob& j : jobs) t += (j.bytes + 255) & ~(size_t)255;
+    return t;
+}
+
+// rl_optimize / rl_lap_eval through the plan cache (see above).  kms[0..2]: HIP-event
+// times of the whole run, the min-curvature and the min-time kernel (-1 if not run).
+int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
+               int32_t modes, const double* centers, const double* Ls, rl_out* out_mc, rl_out* out_mt, float* kms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    g_last_kernel_ms = g_last_call_ms = -1.0f;
+    if (int rc = check_inputs(prob, cfg, n_cfg, B, modes, centers)) return rc;
+    int ndev = 0, dev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ndev) dev = 0;
+    CacheEntry key;
+    key.device = dev;
+    key.N = prob->N;
+    key.B = B;
+    key.ncfg = n_cfg;
+    key.mo = cfg[0].max_outer_iters;
+    key.closed = prob->closed ? 1 : 0;
+    key.Ei = prob->Ei;
+    key.Eo = prob->Eo;
+    key.stream = use_stream(prob->N);
+    key.centers = centers != nullptr;
+    key.Ls = Ls != nullptr;
+    key.segs.assign(prob->inner_seg, prob->inner_seg + 4 * (size_t)prob->Ei);
+    key.segs.insert(key.segs.end(), prob->outer_seg, prob->outer_seg + 4 * (size_t)prob->Eo);
+    PlanCache& pc = plan_cache();
+    CacheEntry* e = pc.take(key);
+    const size_t N2 = 2 * (size_t)std::max(prob->N, 1);
+    const size_t up_ctr = prob->N > 0 ? (centers ? (size_t)B : 1) * N2 * sizeof(double) : 0;
+    const size_t up_ls = Ls ? (size_t)B * sizeof(double) : 0;
+    const size_t up_cfg = (size_t)n_cfg * sizeof(rl_cfg), up_seed = (size_t)B * sizeof(uint64_t);
+    const size_t up_bytes = ((up_ctr + 255) & ~(size_t)255) + ((up_ls + 255) & ~(size_t)255) +
+                            ((up_cfg + 255) & ~(size_t)255) + up_seed;
+    int rc = RL_OK;
+    auto drop = [&](int code) {
+        const std::string msg = g_err;
+        destroy_entry(e);
+        g_err = msg;
+        return code;
+    };
+    if (!e) {
+        rl_plan* p = nullptr;
+        if ((rc = plan_create_ex(&p, dev, prob, cfg, n_cfg, seeds, B, modes, centers, Ls))) return rc;
+        e = new CacheEntry(std::move(key));
+        e->p = p;
+        for (hipEvent_t& v : e->ev)
+            if (hipEventCreateWithFlags(&v, hipEventDisableTiming) != hipSuccess) return drop(fail(RL_EHIP, "hipEventCreate failed"));
+    } else {
+        rl_plan* p = e->p;
+        if (hipSetDevice(p->device) != hipSuccess) return drop(fail(RL_EHIP, "hipSetDevice failed"));
+        for (int m = 0; m < 2; ++m)
+            if ((modes & (1 << m)) && (rc = alloc_mode(p, m))) return drop(rc);
+        p->L = prob->L;
+        p->veh_width = prob->veh_width;
+        if ((rc = ensure_pinned(e, up_bytes))) return drop(rc);
+        hipStream_t st = p->own_stream;
+        size_t off = 0;
+        auto up = [&](void* d, const void* h, size_t bytes) -> bool {
+            if (!bytes) return true;
+            std::memcpy(e->pin + off, h, bytes);
+            const bool ok = hipMemcpyAsync(d, e->pin + off, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+            off += (bytes + 255) & ~(size_t)255;
+            return ok;
+        };
+        std::vector<uint64_t> sd;
+        if (!seeds) sd.assign((size_t)B, 0);
+        if (!up(p->d_center, centers ? centers : prob->center_xy, up_ctr) || !up(p->d_Ls, Ls, up_ls) ||
+            !up(p->d_cfg, cfg, up_cfg) || !up(p->d_seeds, seeds ? seeds : sd.data(), up_seed))
+            return drop(fail(RL_EHIP, "upload (staged) failed"));
+    }
+    rl_plan* p = e->p;
+    p->modes = modes;
+    std::vector<CopyJob> jobs;
+    out_jobs(p, 0, (modes & RL_MODE_MINCURV) ? out_mc : nullptr, jobs);
+    out_jobs(p, 1, (modes & RL_MODE_MINTIME) ? out_mt : nullptr, jobs);
+    // the staging area serves the uploads first, then (stream-ordered after the kernel)
+    // the downloads; a reallocation waits for the uploads already queued
+    const size_t down_bytes = staged_bytes(jobs);
+    if (down_bytes > e->pin_bytes) {
+        if (hipStreamSynchronize(p->own_stream) != hipSuccess) return drop(fail(RL_EHIP, "upload sync"));
+        if ((rc = ensure_pinned(e, down_bytes))) return drop(rc);
+    }
+    if ((rc = rl_plan_run(p, nullptr))) return drop(rc);
+    if ((rc = download_staged(e, p->own_stream, jobs, 0))) return drop(rc);
+    if (hipStreamSynchronize(p->own_stream) != hipSuccess) return drop(fail(RL_EHIP, "stream sync"));
+    float ms[3] = {-1.0f, -1.0f, -1.0f};
+    for (int i = 0; i < 3; ++i) {
+        const bool has = i == 0 || (i == 1 && (modes & RL_MODE_MINCURV)) || (i == 2 && (modes & RL_MODE_MINTIME));
+        if (has && (rc = rl_plan_kernel_ms(p, i, &ms[i]))) return drop(rc);
+    }
+    if (kms) std::memcpy(kms, ms, sizeof(ms));
+    pc.give(e);
+    g_last_kernel_ms = ms[0];
+    g_last_call_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
                 rl_out* out_mincurv, rl_out* out_mintime) {
     int modes = (out_mincurv ? RL_MODE_MINCURV : 0) | (out_mintime ? RL_MODE_MINTIME : 0);
     if (!modes) return fail(RL_EINVAL, "no output requested");
+    return run_cached(prob, cfg, n_cfg, seeds, B, modes, nullptr, nullptr, out_mincurv, out_mintime, nullptr);
+}
+
+int rl_last_call_ms(float* kernel_ms, float* call_ms) {
+    if (g_last_call_ms < 0.0f) return fail(RL_EINVAL, "no successful rl_optimize / rl_lap_eval on this thread");
+    if (kernel_ms) *kernel_ms = g_last_kernel_ms;
+    if (call_ms) *call_ms = g_last_call_ms;
+    return RL_OK;
+}
+
+int rl_release_plan_cache(void) {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    rl_plan* p = nullptr;
-    int rc = rl_plan_create(&p, dev, prob, cfg, n_cfg, seeds, B, modes);
-    if (rc) return rc;
-    rc = rl_plan_run(p, nullptr);
-    if (!rc) rc = rl_plan_fetch(p, out_mincurv, out_mintime);
-    rl_plan_destroy(p);
-    return rc;
+    const bool have = hipGetDevice(&dev) == hipSuccess;
+    plan_cache().clear();
+    if (have) hipSetDevice(dev);
+    return RL_OK;
 }
 
 // rl_optimize over several devices (SURVEY §8b device list, §8e): contiguous instance
@@ -827,19 +1151,19 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, 
                       const int32_t* devices, int32_t n_dev, rl_out* out_mincurv, rl_out* out_mintime) {
     int modes = (out_mincurv ? RL_MODE_MINCURV : 0) | (out_mintime ? RL_MODE_MINTIME : 0);
     if (!modes) return fail(RL_EINVAL, "no output requested");
-    if (!prob || !cfg) return fail(RL_EINVAL, "problem/cfg is NULL");
-    if (B < 1) return fail(RL_EINVAL, "B must be >= 1");
-    if (n_cfg != 1 && n_cfg != B) return fail(RL_EINVAL, "n_cfg must be 1 or B");
     if (n_dev < 1) return fail(RL_EINVAL, "n_dev must be >= 1");
+    // every cfg (all blocks) is checked up front: the output offsets below use cfg[0]'s
+    // max_outer_iters for every block
+    if (int rc0 = check_inputs(prob, cfg, n_cfg, B, modes, nullptr)) return rc0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
     std::vector<int> devs((size_t)n_dev);
     for (int d = 0; d < n_dev; ++d) {
         devs[d] = devices ? devices[d] : d;
         if (devs[d] < 0 || devs[d] >= ndev) return fail(RL_ENODEV, "device index out of range");
-        for (int e = 0; e < d; ++e)
-            if (devs[e] == devs[d]) return fail(RL_EINVAL, "device listed twice");
     }
+    int cur = 0;
+    const bool restore = hipGetDevice(&cur) == hipSuccess;
     const int nb = std::min(n_dev, B);             // no empty blocks
     const int mo = cfg[0].max_outer_iters;
     const size_t N = (size_t)std::max(prob->N, 0);
@@ -847,6 +1171,7 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, 
     auto release = [&](int code) {
         std::string e = g_err;
         for (rl_plan* q : plans) rl_plan_destroy(q);
+        if (restore) hipSetDevice(cur);
         g_err = e;
         return code;
     };

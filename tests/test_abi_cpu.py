@@ -169,5 +169,19 @@ def test_optimize_multi_argument_errors():
     assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 2, None, 0, C.byref(out), None) == abi.RL_EINVAL
     assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 0, None, 1, C.byref(out), None) == abi.RL_EINVAL
     assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 2, None, 1, None, None) == abi.RL_EINVAL
+    # per-instance cfgs whose max_outer_iters differ (a later block with more outer
+    # iterations would write past the caller's [B][max_outer_iters] counters): rejected
+    # before any device work, like rl_optimize
+    cfgs = [O.case_cfg(case) for _ in range(4)]
+    cfgs[3].max_outer_iters = 20
+    arr4, n4 = abi.cfg_array(cfgs)
+    out4 = abi.Outputs.alloc(4, O.case_problem(case).N, 14, False).as_c()
+    assert lib.rl_optimize_multi(C.byref(p), arr4, n4, None, 4, None, 2, C.byref(out4), None) == abi.RL_EINVAL
+    assert b"max_outer_iters" in lib.rl_last_error()
+    cfgs[3].max_outer_iters = 14
+    cfgs[2].max_inner_iters = -1
+    arr4, n4 = abi.cfg_array(cfgs)
+    assert lib.rl_optimize_multi(C.byref(p), arr4, n4, None, 4, None, 2, C.byref(out4), None) == abi.RL_EINVAL
+    assert lib.rl_optimize(C.byref(p), arr4, n4, None, 4, C.byref(out4), None) == abi.RL_EINVAL
     if lib.rl_device_count() == 0:
         assert lib.rl_optimize_multi(C.byref(p), arr, n, None, 2, None, 1, C.byref(out), None) == abi.RL_ENODEV

@@ -573,6 +573,15 @@ def _corridor_cases():
     outer = np.stack([center[sel, 0] + 1.7 * nx[sel], center[sel, 1] + 1.7 * ny[sel]], axis=1)
     out.append(("vertex_rays_far", abi.Problem(center=center, L=1.0, inner_seg=raceline.ring_edges(inner),
                                                outer_seg=raceline.ring_edges(outer), veh_width=0.6, closed=True)))
+    # a NaN ring coordinate (either sign bit): the side filter takes every pair of that
+    # ring as a candidate, and the exact expressions ignore the NaN segments like the
+    # reference's (no hit, std::min keeps the running minimum)
+    for which, j, val in (("inner", 0, np.nan), ("outer", 3, -np.nan), ("outer", 1, np.inf)):
+        kw = dict(center=base.center, L=base.L, inner_seg=base.inner_seg.copy(), outer_seg=base.outer_seg.copy(),
+                  veh_width=base.veh_width, closed=True)
+        kw[f"{which}_seg"][17, j] = val
+        kw[f"{which}_seg"][18, j % 2] = val           # the next segment's start: the same vertex
+        out.append((f"{which}.nonfinite{j}", abi.Problem(**kw)))
     return out
 
 
@@ -610,25 +619,70 @@ def test_c5_oval_seeds_vs_oracle(variant):
         assert omc.accepts.min() > 0 and (omc.evals > omc.accepts + 1).any()   # the path under test ran
 
 
-def test_optimize_multi_one_device_equals_single():
-    """rl_optimize_multi (device list) in its one-device form: the same
-    results as rl_optimize, bit for bit; bad device lists are errors."""
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_optimize_multi_equals_single(devices):
+    """rl_optimize_multi (device list): one block, and three contiguous
+    blocks (B=5 -> 1/2/2 instances, three plans on device 0) with per-instance cfgs, so
+    the per-block cfg/seed slicing and every output offset (x.., lap, evals, accepts,
+    vpass_sweeps) run; the results equal rl_optimize's bit for bit.  Bad device lists
+    and mismatched cfgs are errors, and the caller's current device is kept."""
     lib = _lib_or_skip()
     case = O.load_case("track_competition_map2")
     prob, cfg = O.case_problem(case), O.case_cfg(case)
     seeds = np.arange(5, dtype=np.uint64)
-    mc1, mt1 = raceline.optimize_batch(prob, cfg, seeds, 5)
-    mc2, mt2 = raceline.optimize_batch(prob, cfg, seeds, 5, devices=[0])
+    cfgs = []
+    for k in range(5):
+        c = abi.RlCfg.from_dict(cfg.to_dict())
+        abi.set_mu(c, 1.0 + 0.05 * k)
+        cfgs.append(c)
+    mc1, mt1 = raceline.optimize_batch(prob, cfgs, seeds, 5)
+    mc2, mt2 = raceline.optimize_batch(prob, cfgs, seeds, 5, devices=devices)
     for a, b in ((mc1, mc2), (mt1, mt2)):
         for f in abi.OUT_F64 + ("evals", "accepts"):
             np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
-    np.testing.assert_array_equal(mt1.lap, mt2.lap)
-    with pytest.raises(raceline.RacelineError) as ei:
-        raceline.optimize_batch(prob, cfg, seeds, 5, devices=[0, 0])
-    assert ei.value.code == abi.RL_EINVAL
+    for f in ("v", "ax", "lap", "vpass_sweeps"):
+        np.testing.assert_array_equal(getattr(mt1, f), getattr(mt2, f), err_msg=f)
     with pytest.raises(raceline.RacelineError) as ei:
         raceline.optimize_batch(prob, cfg, seeds, 5, devices=[lib.rl_device_count()])
     assert ei.value.code == abi.RL_ENODEV
+    bad = [abi.RlCfg.from_dict(cfg.to_dict()) for _ in range(5)]
+    bad[3].max_outer_iters = 20          # a later block with more outer iterations
+    with pytest.raises(raceline.RacelineError) as ei:
+        raceline.optimize_batch(prob, bad, seeds, 5, devices=devices)
+    assert ei.value.code == abi.RL_EINVAL
+
+
+def test_dropin_plan_cache_reuse_is_exact():
+    """rl_optimize's plan cache (the reference's one-call-per-track use): repeated calls
+    with the same rings reuse the device plan and pinned staging; the centreline, cfg and
+    seeds of each call are uploaded again, so alternating problems, modes, seeds and cfgs
+    give exactly the results of a fresh plan.  rl_last_call_ms splits kernel and call."""
+    lib = _lib_or_skip()
+    lib.rl_release_plan_cache()
+    case = O.load_case("track_competition_map2")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    other = abi.Problem(center=prob.center[::-1].copy(), L=prob.L * 1.01, inner_seg=prob.inner_seg,
+                        outer_seg=prob.outer_seg, veh_width=prob.veh_width, closed=True)
+    c2 = abi.RlCfg.from_dict(cfg.to_dict())
+    abi.set_mu(c2, 0.9)
+    runs = [(prob, cfg, [0, 3], True, False), (prob, cfg, [0, 3], False, True), (other, c2, [5, 6], True, True),
+            (prob, c2, [0, 3], True, True), (prob, cfg, [0, 3], True, True)]
+    got = []
+    for pr, c, s, mc, mt in runs:
+        got.append(raceline.optimize_batch(pr, c, s, 2, mincurv=mc, mintime=mt))
+        k, w = C.c_float(), C.c_float()
+        assert lib.rl_last_call_ms(C.byref(k), C.byref(w)) == 0 and 0 < k.value <= w.value
+    for (pr, c, s, mc, mt), (gmc, gmt) in zip(runs, got):
+        lib.rl_release_plan_cache()                      # a fresh plan for the reference values
+        fmc, fmt = raceline.optimize_batch(pr, c, s, 2, mincurv=mc, mintime=mt)
+        for g, f in ((gmc, fmc), (gmt, fmt)):
+            if f is None:
+                continue
+            for name in abi.OUT_F64 + ("evals", "accepts"):
+                np.testing.assert_array_equal(getattr(g, name), getattr(f, name), err_msg=name)
+        if fmt is not None:
+            np.testing.assert_array_equal(gmt.lap, fmt.lap)
+            np.testing.assert_array_equal(gmt.v, fmt.v)
 
 
 def test_empty_plan_reports_kernel_time():
