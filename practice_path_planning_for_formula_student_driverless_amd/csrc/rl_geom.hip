@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void rl_geom_kernel(GeomParams g) {
     double x, xp, xpp, y, yp, ypp;
     spline_eval_d(g.kx, g.nk, si, x, xp, xpp);
     spline_eval_d(g.ky, g.nk, si, y, yp, ypp);
-    const double heading = atan2(yp, xp);
+    const double heading = atan2_cr(yp, xp);   // correctly rounded (rl_math.h)
     const double speed2 = xp * xp + yp * yp;
     const double denom = pow15(smax(1e-12, speed2));
     const double curv = (xp * ypp - yp * xpp) / denom;

@@ -67,6 +67,8 @@ __device__ unsigned long long rl_dbg_stamps[16384][8];
 // temporaries competed with the kernel's live state for registers (min-time (8,256):
 // 328 -> 192 B/lane scratch); the default power 2 never calls it
 __device__ __attribute__((noinline)) double pow_noinline(double x, double y) { return pow(x, y); }
+// heading (ref:616), correctly rounded (rl_math.h atan2_cr), out of line for the same reason
+__device__ __attribute__((noinline)) double atan2_noinline(double y, double x) { return atan2_cr(y, x); }
 
 // ------------------------------------------------------------ wave primitives
 // x from another lane for patterns where every lane has a source (quad_perm, row_ror):
@@ -880,7 +882,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             for (int k = 0; k < K; ++k) {
                 double xp, yp, xpp, ypp;
                 deriv(px, py, k, xp, yp, xpp, ypp);
-                double hdv = (outer == MO) ? atan2(yp, xp) : 0.0;   // heading is an output only
+                double hdv = (outer == MO) ? atan2_noinline(yp, xp) : 0.0;   // heading is an output only
                 double denom = pow15(smax(1e-12, xp * xp + yp * yp));
                 double kav = (xp * ypp - yp * xpp) / denom;
                 hd[k] = (k < cnt) ? hdv : 0.0;

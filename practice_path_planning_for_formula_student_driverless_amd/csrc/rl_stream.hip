@@ -75,6 +75,10 @@ struct SSmem {
     double bc[4];
 };
 
+// heading (ref:616), correctly rounded (rl_math.h); out of line so its double-double
+// temporaries do not compete with the kernel's live state for registers
+__device__ __attribute__((noinline)) double atan2_stream(double y, double x) { return atan2_cr(y, x); }
+
 // block sum of NV values; ends with every thread holding the totals
 template <int NV>
 __device__ __forceinline__ void block_sum_s(SSmem& sm, double (&v)[NV], int lane, int wid) {
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 double xp, yp, xpp, ypp;
                 deriv(i, xp, yp, xpp, ypp);
                 KA[i] = (xp * ypp - yp * xpp) / pow15(smax(1e-12, xp * xp + yp * yp));
-                if (outer == MO) p.heading[off + i] = atan2(yp, xp);
+                if (outer == MO) p.heading[off + i] = MT ? atan2_stream(yp, xp) : atan2_cr(yp, xp);   // ref:616
             }
             __syncthreads();
         }

@@ -34,6 +34,21 @@ extern "C" void kat_libm_pow(const double* x, double e, double* y, long n) { for
 extern "C" void kat_libm_hypot(const double* x, const double* y, double* r, long n) {
     for (long i = 0; i < n; ++i) r[i] = hypot(x[i], y[i]);
 }
+extern "C" void kat_atan2(const double* y, const double* x, double* r, long n) {
+    for (long i = 0; i < n; ++i) r[i] = rl::atan2_cr(y[i], x[i]);
+}
+extern "C" void kat_libm_atan2(const double* y, const double* x, double* r, long n) {
+    for (long i = 0; i < n; ++i) r[i] = atan2(y[i], x[i]);
+}
+"""
+
+# the correctly rounded reference: quad-precision atan2q (113-bit significand) rounded
+# to double (a double rounding could only differ within 2^-60 ulp of a midpoint)
+QUAD = r"""
+#include <quadmath.h>
+void kat_quad_atan2(const double* y, const double* x, double* r, long n) {
+    for (long i = 0; i < n; ++i) r[i] = (double)atan2q((__float128)y[i], (__float128)x[i]);
+}
 """
 
 
@@ -57,6 +72,23 @@ def build_shim(d):
     lib.kat_hypot.argtypes = [P, P, P, C.c_long]
     lib.kat_libm_pow.argtypes = [P, C.c_double, P, C.c_long]
     lib.kat_libm_hypot.argtypes = [P, P, P, C.c_long]
+    lib.kat_atan2.argtypes = [P, P, P, C.c_long]
+    lib.kat_libm_atan2.argtypes = [P, P, P, C.c_long]
+    return lib
+
+
+@pytest.fixture(scope="module")
+def quad(tmp_path_factory):
+    d = tmp_path_factory.mktemp("quad")
+    src, so = d / "q.c", d / "libq.so"
+    src.write_text(QUAD)
+    r = subprocess.run(["gcc", "-O2", "-fPIC", "-shared", str(src), "-o", str(so), "-lquadmath"],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        pytest.skip("libquadmath not available")
+    lib = C.CDLL(str(so))
+    P = C.POINTER(C.c_double)
+    lib.kat_quad_atan2.argtypes = [P, P, P, C.c_long]
     return lib
 
 
@@ -179,3 +211,56 @@ def test_hypot_nonfinite(shim):
     glibc = _hyp(shim.kat_libm_hypot, x, y)
     assert np.array_equal(np.isnan(mine), np.isnan(glibc))
     assert np.array_equal(mine[~np.isnan(mine)], glibc[~np.isnan(glibc)])
+
+
+def _atan2_inputs(n, seed):
+    """The hot path's arguments (heading = atan2(y', x'), |x'|, |y'| ~ 1 on unit-speed
+    tracks, every quadrant), a wide exponent spread (ratios down to 2^-1000, both
+    swap branches), near-axis and near-diagonal pairs, and the special values."""
+    rng = np.random.default_rng(seed)
+    m = n // 4
+    a = rng.uniform(0, 2 * np.pi, m)
+    r = rng.uniform(0.5, 1.5, m)
+    ys, xs = [r * np.sin(a)], [r * np.cos(a)]
+    ys.append(rng.choice([-1, 1], m) * 2.0 ** rng.uniform(-60, 60, m))
+    xs.append(rng.choice([-1, 1], m) * 2.0 ** rng.uniform(-60, 60, m))
+    ys.append(rng.choice([-1, 1], m) * 2.0 ** rng.uniform(-1070, 1020, m))
+    xs.append(rng.choice([-1, 1], m) * 2.0 ** rng.uniform(-1070, 1020, m))
+    d = rng.uniform(0.5, 2, m)
+    ys.append(d * (1 + rng.normal(0, 1e-9, m)) * rng.choice([-1, 1], m))     # |y| ~ |x|: t ~ 1
+    xs.append(d * rng.choice([-1, 1], m))
+    inf, nan = np.inf, np.nan
+    sp = [0.0, -0.0, 1.0, -1.0, inf, -inf, nan, 5e-324, -5e-324, 1.7976931348623157e308, 2.0 ** -1022]
+    ys.append(np.array([a for a in sp for _ in sp]))
+    xs.append(np.array([b for _ in sp for b in sp]))
+    return np.concatenate(ys), np.concatenate(xs)
+
+
+def test_atan2_correctly_rounded(shim, quad):
+    """atan2_cr is the correctly rounded atan2 (quad-precision reference) on every
+    input, signed zeros, infinities and NaN included."""
+    y, x = _atan2_inputs(1_000_000, 3)
+    mine = _hyp(shim.kat_atan2, y, x)
+    q = _hyp(quad.kat_quad_atan2, y, x)
+    nan = np.isnan(q)
+    assert np.array_equal(np.isnan(mine), nan)
+    bad = np.nonzero(mine[~nan].view(np.int64) != q[~nan].view(np.int64))[0]
+    assert len(bad) == 0, f"{len(bad)} not correctly rounded, first y={y[~nan][bad[:3]]} x={x[~nan][bad[:3]]}"
+
+
+def test_atan2_against_glibc(shim):
+    """glibc 2.35's atan2 keeps only its fast path (the multi-precision fallback was
+    removed in 2.34), so it misrounds near-ties by one ulp: the rate is recorded here and
+    every difference is a single ulp; special values agree exactly."""
+    y, x = _atan2_inputs(1_000_000, 4)
+    mine = _hyp(shim.kat_atan2, y, x)
+    glibc = _hyp(shim.kat_libm_atan2, y, x)
+    nan = np.isnan(glibc)
+    assert np.array_equal(np.isnan(mine), nan)
+    diff = np.nonzero(mine[~nan].view(np.int64) != glibc[~nan].view(np.int64))[0]
+    ulps = np.abs(mine[~nan][diff].view(np.int64) - glibc[~nan][diff].view(np.int64))
+    rate = len(diff) / len(y)
+    assert rate < 1e-3 and np.all(ulps == 1), (rate, ulps.max() if len(ulps) else 0)
+    tail = len(y) - 121                                   # the special-value block
+    assert np.array_equal(mine[tail:][~nan[tail:]].view(np.int64), glibc[tail:][~nan[tail:]].view(np.int64))
+    print(f"atan2_cr vs glibc atan2: {len(diff)} of {len(y)} differ ({rate:.4%}), all by 1 ulp")
