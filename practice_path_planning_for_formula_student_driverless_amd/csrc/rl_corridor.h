@@ -399,14 +399,21 @@ __device__ __forceinline__ void ring_vertex_ub(const RingDesc& R, const double (
 // (std::min returns the same value on ties), so md_r is searched only within
 // rad = min(ub, s_max) and reported as +inf when it exceeds it.
 // Inactive samples (act false) do no exact work; the caller zeroes their outputs.
-template <int CK, bool TIGHT = true, bool PRUNE = true>
+// phase hook of the diagnostic stamp builds (RL_STAMPS): called with 8 after the inner
+// ring's rays, 9 after the outer ring's, 10 after the fallback searches
+struct NoStamp {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <int CK, bool TIGHT = true, bool PRUNE = true, class Stamp = NoStamp>
 __device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDesc& Ro, const double (&qx)[CK],
                                                 const double (&qy)[CK], const double (&ux)[CK],
                                                 const double (&uy)[CK], const bool (&act)[CK], double guard,
-                                                double (&lo)[CK], double (&hi)[CK]) {
+                                                double (&lo)[CK], double (&hi)[CK], Stamp stamp = Stamp()) {
     double bp[2][CK], bn[2][CK], ub2[2][CK];
     ring_rays<CK>(Ri, qx, qy, ux, uy, act, bp[0], bn[0], ub2[0]);
+    stamp(8);
     ring_rays<CK>(Ro, qx, qy, ux, uy, act, bp[1], bn[1], ub2[1]);
+    stamp(9);
     double md[2][CK];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -439,6 +446,7 @@ __device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDe
         }
         ring_mindist<CK, TIGHT, PRUNE>(R, qx, qy, need, rad, md[r]);
     }
+    stamp(10);
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
         double s[2][2];            // [ring][+n, -n]

@@ -50,7 +50,7 @@ constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per
 // Diagnostic build only (-DRL_STAMPS=1): per-phase s_memtime totals of each
 // workgroup's wave 0, written to a device array no other code reads.
 #ifdef RL_STAMPS
-__device__ unsigned long long rl_dbg_stamps[16384][8];
+__device__ unsigned long long rl_dbg_stamps[16384][16];
 #define RL_STAMP(slot)                                              \
     do {                                                            \
         __builtin_amdgcn_sched_barrier(0);                          \
@@ -202,6 +202,12 @@ __device__ __forceinline__ void put(double (&a)[K], int idx, double v) {
     }
 }
 
+// compile-time flag for generic lambdas (general vs interior stencil forms)
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
 template <int K, int T>
 struct alignas(16) Smem {
     static constexpr int NW = T / 64;
@@ -219,6 +225,7 @@ struct alignas(16) Smem {
     double red[3][NW];           // per-wave partial sums of an evaluation
     double red2[2][NW];          // other block reductions
     double bc[4];                // broadcast scalars
+    int ctr;                     // corridor work queue: next chunk of 64*CK samples
     VConst vc;                   // v-pass constants (read per v pass: no registers held across the kernel)
     union {
         double2 coef[2][K][T];   // [0]: (A1,A2)  [1]: (N0,W)   (precompute_lin_geom_generic)
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     constexpr int NW = T / 64;
     __shared__ Smem<K, T> sm;
 #ifdef RL_STAMPS
-    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_acc[16] = {};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -314,6 +321,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const bool part_wave = RAGGED && (cntL != K) && (((Ta - 1) >> 6) == wid_u);
     // wave-uniform: this wave holds the last active thread or lies beyond it
     const bool tail_wave = wid_u >= ((Ta - 1) >> 6);
+    // Open tracks: the boundary forms of DiffOpsOpen (ref:560-579) apply to samples 0, 1,
+    // N-2 and N-1 only.  A wave none of whose lanes holds one of them evaluates the
+    // interior forms, without the per-sample index tests and coefficient selects; the
+    // (at most two) edge waves keep the general forms.  Wave-uniform.
+    const bool lane_edge = !CLOSED && active && !(base >= 2 && base + K <= N - 2);
+    const bool edge_wave = !CLOSED && __builtin_amdgcn_ballot_w64(lane_edge) != 0;
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
@@ -473,8 +486,17 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
         constexpr int CKK = CK < K ? CK : K;
         double2* bnd = &sm.u.coef[0][0][0];
-        for (int c0 = 0; c0 < N; c0 += T * CKK) {
-            const int i0 = c0 + tid * CKK;
+        // Several waves: chunks of 64*CKK samples from a work queue in LDS, so a wave whose
+        // rays are cheap takes the next chunk instead of waiting at the barrier below for
+        // the slowest wave (the bounds of a sample depend only on that sample).
+        for (int c = (NW == 1) ? 0 : -1;; c = (NW == 1) ? c + 1 : -1) {
+            if constexpr (NW > 1) {
+                int q = 0;
+                if (lane == 0) q = atomicAdd(&sm.ctr, 1);
+                c = __builtin_amdgcn_readlane(q, 0);
+            }
+            if (c * 64 * CKK >= N) break;
+            const int i0 = (c * 64 + lane) * CKK;
             double qx[CKK], qy[CKK], ux[CKK], uy[CKK], lc[CKK], hc[CKK];
             bool act[CKK];
 #pragma unroll
@@ -483,8 +505,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                 act[k] = i0 + k < N;
             }
+#ifdef RL_STAMPS
+            RL_STAMP(7);
+            corridor_bounds<CKK, RL_MD_TIGHT != 0, RL_MD_PRUNE != 0>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard,
+                                                                      lc, hc, [&](int s) { RL_STAMP(s); });
+#else
             corridor_bounds<CKK, RL_MD_TIGHT != 0, RL_MD_PRUNE != 0>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard,
                                                                       lc, hc);
+#endif
 #pragma unroll
             for (int k = 0; k < CKK; ++k) {
                 const int i = i0 + k;
@@ -700,11 +728,21 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         if (j + 1 >= 1 && j + 1 <= N - 2) acc += (+invh2_x2) * vp;
         return acc;
     };
-    auto grad_at = [&](int k, double q1m, double q10, double q1p, double q2m, double q20, double q2p, double am,
-                       double a0, double ap) RL_AI -> double {
-        double g1 = d1t_x2(k, q1m, q10, q1p);
-        double g2 = d2t_x2(k, q2m, q20, q2p);
-        double gsm = d1t_at(k, am, a0, ap);
+    // GEN: the general forms (closed, or an open edge wave); otherwise the open interior
+    // forms of the same gathers for 2 <= j <= N-3, term for term: acc = 0.0, then the
+    // products added in the same order (0.0 + x keeps the reference's zero signs)
+    auto grad_at = [&](auto gen, int k, double q1m, double q10, double q1p, double q2m, double q20, double q2p,
+                       double am, double a0, double ap) RL_AI -> double {
+        double g1, g2, gsm;
+        if (CLOSED || decltype(gen)::value) {
+            g1 = d1t_x2(k, q1m, q10, q1p);
+            g2 = d2t_x2(k, q2m, q20, q2p);
+            gsm = d1t_at(k, am, a0, ap);
+        } else {
+            g1 = (0.0 + inv2h_x2 * q1m) + (-inv2h_x2) * q1p;
+            g2 = ((0.0 + invh2_x2 * q2m) + m2invh2_x2 * q20) + invh2_x2 * q2p;
+            gsm = (0.0 + inv2h * am) + (-inv2h) * ap;
+        }
         return (g1 + g2) + lam2 * gsm;
     };
 
@@ -755,21 +793,31 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         fill_pad(a, rv);
         double pJ = 0.0, pJsm = 0.0;
         double jr[K];
+        auto stencil = [&](auto gen) RL_AI {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double2 c01 = A12R ? make_double2(A1r[k], A2r[k]) : sm.u.coef[0][k][tid];   // (A1, A2)
-            const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
-            double am = (k > 0) ? a[k - 1] : lv;
-            double ap = (k + 1 < K) ? a[k + 1] : rv;
-            double x1 = d1_at(k, am, a[k], ap);
-            double x2 = d2_at(k, am, a[k], ap);
-            double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
-            jr[k] = r;
-            double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
-            q1[k] = c01.x * Wz;
-            q2[k] = c01.y * Wz;
-            a1v[k] = x1;
-        }
+            for (int k = 0; k < K; ++k) {
+                const double2 c01 = A12R ? make_double2(A1r[k], A2r[k]) : sm.u.coef[0][k][tid];   // (A1, A2)
+                const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
+                double am = (k > 0) ? a[k - 1] : lv;
+                double ap = (k + 1 < K) ? a[k + 1] : rv;
+                double x1, x2;
+                if (CLOSED || decltype(gen)::value) {
+                    x1 = d1_at(k, am, a[k], ap);
+                    x2 = d2_at(k, am, a[k], ap);
+                } else {                            // open interior: the closed forms (ref:563-575)
+                    x1 = (ap - am) * inv2h;
+                    x2 = (sub2x(ap, a[k]) + am) * invh2;
+                }
+                double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
+                jr[k] = r;
+                double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
+                q1[k] = c01.x * Wz;
+                q2[k] = c01.y * Wz;
+                a1v[k] = x1;
+            }
+        };
+        if (!edge_wave) stencil(BoolC<false>{});
+        else stencil(BoolC<true>{});
         auto acc = [&](int k) RL_AI {    // Σ γ²r² (ref:881) / Σ z² (ref:661), Σ a1² (ref:662 / 882)
             pJ = __builtin_fma(MT ? G2[k] * jr[k] : jr[k], jr[k], pJ);
             pJsm = __builtin_fma(a1v[k], a1v[k], pJsm);
@@ -808,11 +856,15 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         fill_pad(q1, r1);
         fill_pad(q2, r2);
         fill_pad(a1v, r3);
+        auto grads = [&](auto gen) RL_AI {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            g[k] = grad_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
-                            (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
-                            (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
+            for (int k = 0; k < K; ++k)
+                g[k] = grad_at(gen, k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
+                               (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
+                               (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
+        };
+        if (!edge_wave) grads(BoolC<false>{});
+        else grads(BoolC<true>{});
     };
 
     // ======================================================================
@@ -857,6 +909,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         if (outer < MO) {
             // normals + corridor (ref:692-711 initially with the veh_width argument,
             // ref:746-756 after each update with cfg veh_width_m)
+            if (tid == 0) sm.ctr = 0;                            // read after the barrier below
             normals();
             __syncthreads();
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
@@ -1070,7 +1123,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #ifdef RL_STAMPS
     RL_STAMP(6);
     if (tid == 0 && b < 16384) {
-        for (int i = 0; i < 8; ++i) rl_dbg_stamps[b][i] = st_acc[i];
+        for (int i = 0; i < 16; ++i) rl_dbg_stamps[b][i] = st_acc[i];
     }
 #endif
 }
@@ -1078,7 +1131,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #ifdef RL_STAMPS
 int debug_stamps(unsigned long long* host, int nblocks) {
     if (nblocks > 16384) nblocks = 16384;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_stamps), sizeof(unsigned long long) * 8 * nblocks) == hipSuccess ? 0 : -3;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_stamps), sizeof(unsigned long long) * 16 * nblocks) == hipSuccess ? 0 : -3;
 }
 #endif
 

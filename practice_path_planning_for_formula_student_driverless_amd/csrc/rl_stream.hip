@@ -73,6 +73,7 @@ struct SSmem {
     double red[RED_SLOTS][NWS];
     double vin[2][TS];
     double bc[4];
+    int ctr;          // corridor work queue: next chunk of 64*RL_SCK samples
 };
 
 // heading (ref:616), correctly rounded (rl_math.h); out of line so its double-double
@@ -101,7 +102,7 @@ __device__ __forceinline__ void block_sum_s(SSmem& sm, double (&v)[NV], int lane
 
 #ifdef RL_STAMPS
 // Diagnostic build only: per-phase s_memtime totals of each workgroup's wave 0
-__device__ unsigned long long rl_dbg_stamps_s[16384][8];
+__device__ unsigned long long rl_dbg_stamps_s[16384][16];
 #define RL_SSTAMP(slot)                                             \
     do {                                                            \
         __builtin_amdgcn_sched_barrier(0);                          \
@@ -118,7 +119,7 @@ template <bool CLOSED, bool MT>
 __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb) {
     __shared__ SSmem sm;
 #ifdef RL_STAMPS
-    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_acc[16] = {};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -353,13 +354,23 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         }
         RL_SSTAMP(5);
         if (outer < MO) {
+            if (tid == 0) sm.ctr = 0;                              // read after the barrier below
             for (int i = tid; i < N; i += TS) normal_at(i);
             __syncthreads();
             RL_SSTAMP(6);
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
 #if RL_SCK > 1
-            // RL_SCK adjacent samples per lane (a wave scans 64*RL_SCK consecutive rays)
-            for (int i0 = RL_SCK * tid; i0 < N; i0 += RL_SCK * TS) {
+            // RL_SCK adjacent samples per lane (a wave scans 64*RL_SCK consecutive rays).
+            // The chunks come from a work queue in LDS: a ray's cost depends on the ring
+            // geometry around it, and a static interleave left the other waves waiting at the
+            // next barrier for the slowest one (C5 phase stamps: 23 % of the kernel).  Each
+            // sample's bounds depend only on that sample, so the assignment does not change them.
+            for (;;) {
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&sm.ctr, 1);
+                c = __builtin_amdgcn_readlane(c, 0);
+                if (c * 64 * RL_SCK >= N) break;
+                const int i0 = (c * 64 + lane) * RL_SCK;
                 double qx[RL_SCK], qy[RL_SCK], ux[RL_SCK], uy[RL_SCK], lk[RL_SCK], hk[RL_SCK];
                 bool act[RL_SCK];
 #pragma unroll
@@ -368,7 +379,13 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                     act[k] = i0 + k < N;
                 }
+#ifdef RL_STAMPS
+                RL_SSTAMP(7);
+                corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk,
+                                        [&](int s) { RL_SSTAMP(s); });
+#else
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
+#endif
 #pragma unroll
                 for (int k = 0; k < RL_SCK; ++k) {
                     const int i = i0 + k;
@@ -638,7 +655,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     }
 #ifdef RL_STAMPS
     if (tid == 0 && b < 16384) {
-        for (int i = 0; i < 8; ++i) rl_dbg_stamps_s[b][i] = st_acc[i];
+        for (int i = 0; i < 16; ++i) rl_dbg_stamps_s[b][i] = st_acc[i];
     }
 #endif
 }
@@ -655,7 +672,7 @@ int debug_counts(unsigned long long* host, int reset) {
 #ifdef RL_STAMPS
 int debug_stamps_stream(unsigned long long* host, int nblocks) {
     if (nblocks > 16384) nblocks = 16384;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_stamps_s), sizeof(unsigned long long) * 8 * nblocks) == hipSuccess ? 0 : -3;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_stamps_s), sizeof(unsigned long long) * 16 * nblocks) == hipSuccess ? 0 : -3;
 }
 #endif
 

@@ -7,7 +7,9 @@ sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "tests"))
 import oracle_lib as O
 from practice_path_planning_for_formula_student_driverless_amd import abi
 lib = abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_stamps.so"))
-names = ["setup", "corridor", "mt:κ/vpass/γ", "lin-geom", "PGD loop", "update", "normals", "-"]
+names = ["setup", "corridor tail (write, seed)", "mt:κ/vpass/γ", "lin-geom", "PGD loop", "update", "normals",
+         "corridor loads", "corridor: inner-ring rays", "corridor: outer-ring rays", "corridor: fallback search",
+         "-", "-", "-", "-", "-"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 case = O.load_case("oval_n10000"); prob = O.case_problem(case); cfg = O.case_cfg(case)
 h = C.c_void_p(); p = prob.as_c(); arr, n = abi.cfg_array(cfg)
@@ -15,10 +17,10 @@ seeds = np.arange(B, dtype=np.uint64)
 assert lib.rl_plan_create(C.byref(h), 0, C.byref(p), arr, n, abi.u64ptr(seeds), B, 1) == 0
 assert lib.rl_plan_run(h, None) == 0
 ms = C.c_float(); lib.rl_plan_kernel_ms(h, 1, C.byref(ms))
-st = np.zeros((B, 8), dtype=np.uint64)
+st = np.zeros((B, 16), dtype=np.uint64)
 assert lib.rl_debug_stamps_stream(st.ctypes.data_as(C.c_void_p), B) == 0
 tot = st.sum(0).astype(float)
 print(f"C5 B={B} kernel {ms.value:.2f} ms; per-block cycles {tot.sum()/B:.3e}")
 for i, nm in enumerate(names):
-    if tot[i] > 0: print(f"   {nm:18s} {100*tot[i]/tot.sum():5.1f}%  {tot[i]/B:.3e} cyc/block")
+    if tot[i] > 0: print(f"   {nm:30s} {100*tot[i]/tot.sum():5.1f}%  {tot[i]/B:.3e} cyc/block")
 lib.rl_plan_destroy(h)
