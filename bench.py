@@ -427,9 +427,32 @@ def run_c5(world, rank, local, dev, dist):
             "model_GBps_aside": round(model / (k_ms * 1e-3) / 1e9, 1),
             "model_note": "SURVEY §8d one-pass-per-evaluation streaming bytes; batched backtracking reads the state "
                           "once per 4 trial steps, so this model is not a roofline for this kernel"}
-    return {"instances": world * B, "N": prob.N, "kernel_ms": round(k_ms, 3),
-            "outer_iters_per_s": round(world * B * 14 / (k_ms * 1e-3), 1), "evals_per_outer": E_k,
-            "roofline": roof, "seed0_vs_reference_max_rel_err": rel}
+    out = {"instances": world * B, "N": prob.N, "kernel_ms": round(k_ms, 3),
+           "outer_iters_per_s": round(world * B * 14 / (k_ms * 1e-3), 1), "evals_per_outer": E_k,
+           "roofline": roof, "seed0_vs_reference_max_rel_err": rel}
+    if rank == 0:
+        out["mintime"] = run_c5_mintime(local, prob, cfg, case, B)
+    return out
+
+
+def run_c5_mintime(local, prob, cfg, case, B):
+    """compute_min_time_raceline (ref:905-1052) at C5's size: the N=10000 oval, B seeds,
+    through the streaming kernel's min-time instantiation (rank 0's own seeds)."""
+    plan = raceline.Plan(prob, cfg, seeds=np.arange(B, dtype=np.uint64), B=B, modes=abi.RL_MODE_MINTIME,
+                         device=local)
+    plan.run()
+    ms = []
+    for _ in range(3):
+        plan.run()
+        ms.append(plan.kernel_ms(2))
+    _, mt = plan.fetch()
+    plan.close()
+    k_ms = float(np.mean(ms))
+    lap_ref = float(case["mt_lap"])
+    return {"instances": B, "kernel_ms": round(k_ms, 3), "outer_iters_per_s": round(B * 14 / (k_ms * 1e-3), 1),
+            "evals_per_outer": float(mt.evals.mean()), "vpass_sweeps_mean": float(mt.vpass_sweeps.mean()),
+            "kernel": "rl_stream_kernel<closed,mintime>", "lap_seed0_s": float(mt.lap[0]),
+            "lap_seed0_vs_reference_rel": abs(float(mt.lap[0]) - lap_ref) / lap_ref}
 
 
 def run_dropin(local):

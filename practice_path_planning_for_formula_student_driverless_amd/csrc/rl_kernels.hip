@@ -202,12 +202,6 @@ __device__ __forceinline__ void put(double (&a)[K], int idx, double v) {
     }
 }
 
-// compile-time flag for generic lambdas (general vs interior stencil forms)
-template <bool B>
-struct BoolC {
-    static constexpr bool value = B;
-};
-
 template <int K, int T>
 struct alignas(16) Smem {
     static constexpr int NW = T / 64;
@@ -321,12 +315,6 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const bool part_wave = RAGGED && (cntL != K) && (((Ta - 1) >> 6) == wid_u);
     // wave-uniform: this wave holds the last active thread or lies beyond it
     const bool tail_wave = wid_u >= ((Ta - 1) >> 6);
-    // Open tracks: the boundary forms of DiffOpsOpen (ref:560-579) apply to samples 0, 1,
-    // N-2 and N-1 only.  A wave none of whose lanes holds one of them evaluates the
-    // interior forms, without the per-sample index tests and coefficient selects; the
-    // (at most two) edge waves keep the general forms.  Wave-uniform.
-    const bool lane_edge = !CLOSED && active && !(base >= 2 && base + K <= N - 2);
-    const bool edge_wave = !CLOSED && __builtin_amdgcn_ballot_w64(lane_edge) != 0;
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
@@ -728,21 +716,11 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         if (j + 1 >= 1 && j + 1 <= N - 2) acc += (+invh2_x2) * vp;
         return acc;
     };
-    // GEN: the general forms (closed, or an open edge wave); otherwise the open interior
-    // forms of the same gathers for 2 <= j <= N-3, term for term: acc = 0.0, then the
-    // products added in the same order (0.0 + x keeps the reference's zero signs)
-    auto grad_at = [&](auto gen, int k, double q1m, double q10, double q1p, double q2m, double q20, double q2p,
-                       double am, double a0, double ap) RL_AI -> double {
-        double g1, g2, gsm;
-        if (CLOSED || decltype(gen)::value) {
-            g1 = d1t_x2(k, q1m, q10, q1p);
-            g2 = d2t_x2(k, q2m, q20, q2p);
-            gsm = d1t_at(k, am, a0, ap);
-        } else {
-            g1 = (0.0 + inv2h_x2 * q1m) + (-inv2h_x2) * q1p;
-            g2 = ((0.0 + invh2_x2 * q2m) + m2invh2_x2 * q20) + invh2_x2 * q2p;
-            gsm = (0.0 + inv2h * am) + (-inv2h) * ap;
-        }
+    auto grad_at = [&](int k, double q1m, double q10, double q1p, double q2m, double q20, double q2p, double am,
+                       double a0, double ap) RL_AI -> double {
+        double g1 = d1t_x2(k, q1m, q10, q1p);
+        double g2 = d2t_x2(k, q2m, q20, q2p);
+        double gsm = d1t_at(k, am, a0, ap);
         return (g1 + g2) + lam2 * gsm;
     };
 
@@ -793,31 +771,21 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         fill_pad(a, rv);
         double pJ = 0.0, pJsm = 0.0;
         double jr[K];
-        auto stencil = [&](auto gen) RL_AI {
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const double2 c01 = A12R ? make_double2(A1r[k], A2r[k]) : sm.u.coef[0][k][tid];   // (A1, A2)
-                const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
-                double am = (k > 0) ? a[k - 1] : lv;
-                double ap = (k + 1 < K) ? a[k + 1] : rv;
-                double x1, x2;
-                if (CLOSED || decltype(gen)::value) {
-                    x1 = d1_at(k, am, a[k], ap);
-                    x2 = d2_at(k, am, a[k], ap);
-                } else {                            // open interior: the closed forms (ref:563-575)
-                    x1 = (ap - am) * inv2h;
-                    x2 = (sub2x(ap, a[k]) + am) * invh2;
-                }
-                double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
-                jr[k] = r;
-                double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
-                q1[k] = c01.x * Wz;
-                q2[k] = c01.y * Wz;
-                a1v[k] = x1;
-            }
-        };
-        if (!edge_wave) stencil(BoolC<false>{});
-        else stencil(BoolC<true>{});
+        for (int k = 0; k < K; ++k) {
+            const double2 c01 = A12R ? make_double2(A1r[k], A2r[k]) : sm.u.coef[0][k][tid];   // (A1, A2)
+            const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
+            double am = (k > 0) ? a[k - 1] : lv;
+            double ap = (k + 1 < K) ? a[k + 1] : rv;
+            double x1 = d1_at(k, am, a[k], ap);
+            double x2 = d2_at(k, am, a[k], ap);
+            double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
+            jr[k] = r;
+            double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
+            q1[k] = c01.x * Wz;
+            q2[k] = c01.y * Wz;
+            a1v[k] = x1;
+        }
         auto acc = [&](int k) RL_AI {    // Σ γ²r² (ref:881) / Σ z² (ref:661), Σ a1² (ref:662 / 882)
             pJ = __builtin_fma(MT ? G2[k] * jr[k] : jr[k], jr[k], pJ);
             pJsm = __builtin_fma(a1v[k], a1v[k], pJsm);
@@ -856,15 +824,11 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         fill_pad(q1, r1);
         fill_pad(q2, r2);
         fill_pad(a1v, r3);
-        auto grads = [&](auto gen) RL_AI {
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                g[k] = grad_at(gen, k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
-                               (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
-                               (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
-        };
-        if (!edge_wave) grads(BoolC<false>{});
-        else grads(BoolC<true>{});
+        for (int k = 0; k < K; ++k)
+            g[k] = grad_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
+                            (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
+                            (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
     };
 
     // ======================================================================

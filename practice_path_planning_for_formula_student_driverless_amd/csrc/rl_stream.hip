@@ -58,7 +58,7 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 }
 
 // backtracking trials evaluated per pass over the state once the first trial of an
-// inner iteration is rejected (min-curv; min-time keeps one per pass)
+// inner iteration is rejected (both optimisers)
 // corridor samples per lane in the streaming kernel (C5 A/B: 1 -> 36.0 ms, 2 -> 32.4 ms,
 // 4 -> 41.6 ms; scripts/ab_c5.py)
 #ifndef RL_SCK
@@ -73,9 +73,13 @@ struct SSmem {
     double red[RED_SLOTS][NWS];
     double vin[2][TS];
     double bc[4];
+    VConst vc;        // v-pass constants (read at the start of each v pass: no registers held)
     int ctr;          // corridor work queue: next chunk of 64*RL_SCK samples
 };
 
+// std::pow for a non-default time_gamma_power (ref:960), out of line: inlined, OCML's pow
+// held registers across the whole kernel (min-time scratch 416 -> 272 B/lane)
+__device__ __attribute__((noinline)) double pow_stream(double x, double y) { return pow(x, y); }
 // heading (ref:616), correctly rounded (rl_math.h); out of line so its double-double
 // temporaries do not compete with the kernel's live state for registers
 __device__ __attribute__((noinline)) double atan2_stream(double y, double x) { return atan2_cr(y, x); }
@@ -243,19 +247,23 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     };
 
     // ---- v(s) profile (ref:782-862), contiguous ranges [t*Cr, t*Cr+Cr) --------
-    VConst vc;
-    vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;
-    vc.a_total2 = vc.a_total * vc.a_total;
-    vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;
-    vc.Fr = C.mass_kg * 9.81 * C.c_rr;
-    vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
-    vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
-    vc.h = h; vc.two_h = two_h;          // two_h = uni(2*h): the same value, from an SGPR pair
+    if (tid == 0) {
+        VConst vc;
+        vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;
+        vc.a_total2 = vc.a_total * vc.a_total;
+        vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;
+        vc.Fr = C.mass_kg * 9.81 * C.c_rr;
+        vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
+        vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
+        vc.h = h; vc.two_h = two_h;      // two_h = uni(2*h): the same value, from an SGPR pair
+        sm.vc = vc;                      // first read after the outer loop's first barrier
+    }
     const int Cr = (N + TS - 1) / TS;
     const int r0 = min(N, tid * Cr), r1 = min(N, r0 + Cr);
     const bool ract = r0 < r1;
     const bool has_left = ract && r0 > 0, has_right = ract && r1 < N;
     auto vpass = [&]() -> int {
+        const VConst vc = sm.vc;
         for (int i = r0; i < r1; ++i) {
             double kk = fabs(KA[i]);
             V[i] = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
@@ -445,7 +453,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     double vkappa = sqrt(C.a_lat_max / smax(fabs(KA[i]), C.kappa_eps));
                     double rr = smin(1.0, V[i] / smax(1e-6, vkappa));
                     double r = smin(1.0, smax(0.0, rr * rr));
-                    double rp = (C.time_gamma_power == 2.0) ? r * r : pow(r, C.time_gamma_power);
+                    double rp = (C.time_gamma_power == 2.0) ? r * r : pow_stream(r, C.time_gamma_power);
                     double corner_w = 1.0 + C.w_time_gain * rp;
                     double invv_w = 1.0;
                     if (C.time_weight_use_inv_v) {
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         // step the arithmetic and the per-thread sample order of eval_trial, and
         // block_sum_s reduces each sum on its own, so J and the decrease of every step
         // are bit-identical to one-at-a-time trials.  Writes nothing.
-        constexpr int MB = MT ? 1 : RL_BT_BATCH;
+        constexpr int MB = RL_BT_BATCH;
         auto eval_trials = [&](const double (&st)[MB], int m, double (&Jn)[MB], double (&dn)[MB]) {
             double s3[3 * MB];
 #pragma unroll
@@ -563,6 +571,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 const double amv = al_p[im], gm = GR[im], lom = LO[im], him = HI[im];
                 const double apv = al_p[ip], gp = GR[ip], lop = LO[ip], hip = HI[ip];
                 const double w = CW[i], A1 = CA1[i], A2 = CA2[i], n0 = CN0[i];
+                const double g2 = MT ? G2[i] : 1.0;
 #pragma unroll
                 for (int j = 0; j < MB; ++j) {
                     if (j < m) {                                      // uniform
@@ -571,7 +580,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         const double ap = (ip == i) ? a0 : smin(hip, smax(lop, apv - st[j] * gp));
                         const double x1 = d1_at(i, am, a0, ap), x2 = d2_at(i, am, a0, ap);
                         const double r = w * (n0 + A1 * x1 + A2 * x2);
-                        s3[3 * j] += r * r;
+                        s3[3 * j] += MT ? g2 * r * r : r * r;        // term_at's jz (ref:881 / 661)
                         s3[3 * j + 1] += x1 * x1;
                         s3[3 * j + 2] += g0 * (a0 - a0v);
                     }

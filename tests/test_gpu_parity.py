@@ -602,13 +602,16 @@ def test_corridor_vs_oracle():
             assert bad.size == 0, f"{name}.{what}: {bad.size} samples differ, first {bad[:5]} {g[bad[:3]]} vs {r[bad[:3]]}"
 
 
+@pytest.mark.parametrize("mode", ["mincurv", "mintime"])
 @pytest.mark.parametrize("variant", ["default", "backtrack_accepts"])
-def test_c5_oval_seeds_vs_oracle(variant):
+def test_c5_oval_seeds_vs_oracle(variant, mode):
     """C5's shape at its real size: the N=10000 oval through the streaming kernel with
-    jittered α-seeds {1, 7} (ref:720 + the seed, corridor updates ref:749-757).  The
-    default cfg rejects every trial (E_k = 21, the bench's C5 path); the second cfg
-    (step_init 1e-3, step_min 1e-15) accepts after backtracking, so the batched-trial
-    accept / step_min cut-off fires at N=10000.  Counters exact, columns within the
+    jittered α-seeds {1, 7} (ref:720 + the seed, corridor updates ref:749-757), for both
+    optimisers (compute_min_time_raceline ref:905-1052 at N > 4096: v-pass, γ², batched
+    backtracking with the time-weighted cost).  The default cfg rejects every trial
+    (E_k = 21, the bench's C5 path); the second cfg (step_init 1e-3, step_min 1e-15)
+    accepts after backtracking, so the batched-trial accept / step_min cut-off fires at
+    N=10000.  Counters (evals, accepts, v-pass sweeps) exact, columns within the
     tolerance, zero signs equal."""
     _lib_or_skip()
     case = O.load_case("oval_n10000")
@@ -616,11 +619,13 @@ def test_c5_oval_seeds_vs_oracle(variant):
     if variant == "backtrack_accepts":
         cfg.step_init, cfg.step_min = 1e-3, 1e-15
         cfg.max_outer_iters, cfg.max_inner_iters = 4, 30
-    mc, _ = raceline.optimize_batch(prob, cfg, [1, 7], 2, mintime=False)
-    omc, _ = O.run_oracle(prob, cfg, seeds=[1, 7], B=2, modes=(True, False))
-    compare_outputs(mc, omc, False, f"c5 {variant}")
+    mt_mode = mode == "mintime"
+    mc, mt = raceline.optimize_batch(prob, cfg, [1, 7], 2, mincurv=not mt_mode, mintime=mt_mode)
+    omc, omt = O.run_oracle(prob, cfg, seeds=[1, 7], B=2, modes=(not mt_mode, mt_mode))
+    got, ref = (mt, omt) if mt_mode else (mc, omc)
+    compare_outputs(got, ref, mt_mode, f"c5 {mode} {variant}")
     if variant == "backtrack_accepts":
-        assert omc.accepts.min() > 0 and (omc.evals > omc.accepts + 1).any()   # the path under test ran
+        assert ref.accepts.min() > 0 and (ref.evals > ref.accepts + 1).any()   # the path under test ran
 
 
 @pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
