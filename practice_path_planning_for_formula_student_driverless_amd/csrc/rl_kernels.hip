@@ -315,6 +315,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const bool part_wave = RAGGED && (cntL != K) && (((Ta - 1) >> 6) == wid_u);
     // wave-uniform: this wave holds the last active thread or lies beyond it
     const bool tail_wave = wid_u >= ((Ta - 1) >> 6);
+    // Open tracks without a partial chunk (OPEN_FAST): the boundary forms of DiffOpsOpen
+    // (ref:560-579) touch samples 0, 1, N-2 and N-1 only, i.e. chunk positions k = 0, 1
+    // of lane 0 and K-2, K-1 of the last active lane.  Every lane evaluates the interior
+    // forms; a wave holding lane 0 or the last active lane (edge_wave, uniform) then
+    // re-evaluates those four positions with the general forms, which equal the interior
+    // ones on every other lane.
+    constexpr bool OPEN_FAST = !CLOSED && !RAGGED;
+    const bool edge_wave = OPEN_FAST && (wid_u == 0 || wid_u == ((Ta - 1) >> 6));
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
@@ -723,6 +731,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         double gsm = d1t_at(k, am, a0, ap);
         return (g1 + g2) + lam2 * gsm;
     };
+    // the same gathers for an open interior sample (2 <= j <= N-3), term for term as the
+    // general forms evaluate them there: acc = 0.0, then the products in the same order
+    // (0.0 + x keeps the reference's zero signs)
+    auto grad_int = [&](double q1m, double q1p, double q2m, double q20, double q2p, double am, double ap) RL_AI
+        -> double {
+        const double g1 = (0.0 + inv2h_x2 * q1m) + (-inv2h_x2) * q1p;
+        const double g2 = ((0.0 + invh2_x2 * q2m) + m2invh2_x2 * q20) + invh2_x2 * q2p;
+        const double gsm = (0.0 + inv2h * am) + (-inv2h) * ap;
+        return (g1 + g2) + lam2 * gsm;
+    };
 
     // ---- state ------------------------------------------------------------
     double G2[K];                                   // γ² (min-time)
@@ -740,8 +758,11 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #ifndef RL_A12_REG
 #define RL_A12_REG 2
 #endif
-    constexpr bool A12R = RL_A12_REG && !MT && (CLOSED || K < 8);   // (A1, A2) in registers instead of LDS
-    constexpr bool N0R = A12R && RL_A12_REG >= 2;                    // and N0
+#ifndef RL_A12_MT
+#define RL_A12_MT 0      // min-time: 0 none, 1 N0, 2 A1+A2, 3 all three in registers (A/B knob)
+#endif
+    constexpr bool A12R = (RL_A12_REG && !MT && (CLOSED || K < 8)) || (MT && CLOSED && (RL_A12_MT & 2));   // (A1, A2) in registers instead of LDS
+    constexpr bool N0R = (A12R && !MT && RL_A12_REG >= 2) || (MT && CLOSED && (RL_A12_MT & 1));            // and N0
     double A1r[K], A2r[K], N0r[K];
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
@@ -777,8 +798,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
             double am = (k > 0) ? a[k - 1] : lv;
             double ap = (k + 1 < K) ? a[k + 1] : rv;
-            double x1 = d1_at(k, am, a[k], ap);
-            double x2 = d2_at(k, am, a[k], ap);
+            double x1, x2;
+            if (OPEN_FAST && !(edge_wave && (k == 0 || k == K - 1))) {   // interior forms (ref:563-575)
+                x1 = (ap - am) * inv2h;
+                x2 = (sub2x(ap, a[k]) + am) * invh2;
+            } else {
+                x1 = d1_at(k, am, a[k], ap);
+                x2 = d2_at(k, am, a[k], ap);
+            }
             double r = c23.y * (c23.x + c01.x * x1 + c01.y * x2);
             jr[k] = r;
             double Wz = MT ? (c23.y * G2[k] * r) : (c23.y * r);
@@ -825,10 +852,15 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         fill_pad(q2, r2);
         fill_pad(a1v, r3);
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            g[k] = grad_at(k, (k > 0) ? q1[k - 1] : l1, q1[k], (k + 1 < K) ? q1[k + 1] : r1,
-                            (k > 0) ? q2[k - 1] : l2, q2[k], (k + 1 < K) ? q2[k + 1] : r2,
-                            (k > 0) ? a1v[k - 1] : l3, a1v[k], (k + 1 < K) ? a1v[k + 1] : r3);
+        for (int k = 0; k < K; ++k) {
+            const double q1m = (k > 0) ? q1[k - 1] : l1, q1p = (k + 1 < K) ? q1[k + 1] : r1;
+            const double q2m = (k > 0) ? q2[k - 1] : l2, q2p = (k + 1 < K) ? q2[k + 1] : r2;
+            const double am = (k > 0) ? a1v[k - 1] : l3, ap = (k + 1 < K) ? a1v[k + 1] : r3;
+            if (OPEN_FAST && !(edge_wave && (k < 2 || k >= K - 2)))
+                g[k] = grad_int(q1m, q1p, q2m, q2[k], q2p, am, ap);
+            else
+                g[k] = grad_at(k, q1m, q1[k], q1p, q2m, q2[k], q2p, am, a1v[k], ap);
+        }
     };
 
     // ======================================================================

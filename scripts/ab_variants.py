@@ -34,7 +34,8 @@ def fetch(lib, h, B, N, mo, mt):
 
 res = {}
 CASES = [("C2", "cmap1_n2000", 1024, 1, 1, False), ("C3mt", "cmap1_n2000_vp20", 256, 2, 2, True),
-         ("C5", "oval_n10000", 1024, 1, 1, False)]
+         ("C3big", "cmap1_n2000_vp20", 4096, 2, 2, True), ("C5", "oval_n10000", 1024, 1, 1, False),
+         ("C5mt", "oval_n10000", 1024, 2, 2, True)]
 sel = os.environ.get("AB_CASES")
 for cname, cfgname, B, modes, idx, mt in [c for c in CASES if not sel or c[0] in sel.split(",")]:
     case = O.load_case(cfgname); prob = O.case_problem(case); cfg = O.case_cfg(case)

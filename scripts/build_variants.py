@@ -27,6 +27,9 @@ VARIANTS = {
     "a12_0": {"RL_A12_REG": 0},
     "a12_1": {"RL_A12_REG": 1},
     "a12_2": {"RL_A12_REG": 2},
+    "a12mt1": {"RL_A12_MT": 1},
+    "a12mt2": {"RL_A12_MT": 2},
+    "a12mt3": {"RL_A12_MT": 3},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }

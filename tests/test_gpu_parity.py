@@ -742,3 +742,36 @@ def test_device_libm_known_answers(tmp_path):
     assert ulps.max() <= 1 and np.count_nonzero(ulps) <= 2e-3 * ulps.size, (ulps.max(), np.count_nonzero(ulps))
     print(f"atan2: device == host atan2_cr on all {ulps.size} headings; {np.count_nonzero(ulps)} differ from "
           f"glibc by 1 ulp (glibc misrounds), the rest equal")
+
+
+def test_c4_grid_concurrent_streams_vs_oracle():
+    """C4's schedule (bench.run_c4): one plan per track with per-instance sweep cfgs
+    (mu with a_total_max recomputed, P_max_W, lambda_smooth from distributed.c4_grid), all
+    plans enqueued on concurrent HIP streams before any wait.  Two tracks x 64 grid points
+    (every 8th point of the 512-point grid): laps within 1e-4 (measured on the bench's full
+    grid: <= 2.4e-8 s), every counter exact."""
+    import torch
+
+    from practice_path_planning_for_formula_student_driverless_amd import distributed as D
+
+    _lib_or_skip()
+    base = O.case_cfg(O.load_case("track_training_map"))
+    cfgs = D.c4_cfgs(base)
+    pts = list(range(0, 512, 8))
+    plans, probs = [], []
+    for t in ("competition_map1", "competition_map_testday3"):
+        prob = O.case_problem(O.load_case("track_" + t))
+        plans.append(raceline.Plan(prob, [cfgs[k] for k in pts], B=len(pts),
+                                   modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME))
+        probs.append(prob)
+    streams = [torch.cuda.Stream() for _ in plans]
+    for pl, st in zip(plans, streams):
+        pl.run(st.cuda_stream)
+    for st in streams:
+        st.synchronize()
+    for pl, prob in zip(plans, probs):
+        mc, mt = pl.fetch()
+        pl.close()
+        omc, omt = O.run_oracle(prob, [cfgs[k] for k in pts], B=len(pts))
+        compare_outputs(mc, omc, False, "c4.mc")
+        compare_outputs(mt, omt, True, "c4.mt")
