@@ -558,46 +558,60 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #pragma unroll
             for (int k = 0; k < K; ++k) vstart[k] = v[k];
             // ---- forward pass (ref:829-833)
-            // A chunk re-evaluated with a new incoming value stops as soon as a value equals,
-            // bit for bit, the one it already holds from its previous evaluation in this pass:
-            // the rest of the chunk and its outgoing value would repeat (each step depends only
-            // on the previous value).  The wave stops when all its lanes have.  The relaxation
-            // ends when no published value changed.
+            // Exact chunked relaxation.  Every chunk first evaluates with no incoming constraint;
+            // then, within each wave, a lane takes its left neighbour's outgoing value by DPP
+            // (lane 0 the previous wave's, through LDS) and re-evaluates while that value
+            // changes: the in-wave rounds need no barrier, and one barrier per round across
+            // waves passes the wave edges on until no published edge changes.  A chunk
+            // re-evaluated with a new incoming value stops as soon as a value equals, bit for
+            // bit, the one it already holds (each step depends only on the previous value), so
+            // its outgoing value would repeat.  Each chunk's result is a deterministic function
+            // of its incoming value, so the fixed point is the serial result bit for bit.
             {
                 double in_prev = -1.0;       // sentinel (valid values are >= 0 or +inf)
-                double out = 0.0;            // the value this chunk publishes
-                for (int it = 0;; ++it) {
-                    double in = INFINITY;    // first iteration: no incoming constraint
-                    if (it > 0 && has_left) in = sm.u.vin[(it - 1) & 1][tid - 1];
-                    bool changed = false;
-                    if (active && in != in_prev) {
-                        in_prev = in;
-                        double cur = vstart[0];
-                        if (has_left) cur = smin(vstart[0], in);     // v[i+1] = min(v[i+1], vf)
-                        bool go = (it == 0) || !same_bits(cur, v[0]);
-                        v[0] = cur;
+                double out = INFINITY;       // the value this chunk passes right
+                double wave_in = INFINITY;   // lane 0: the previous wave's last outgoing value
+                double pub = -1.0;           // lane 63: the value last published for the next wave
+                bool first = true;
+                for (int ro = 0;; ++ro) {
+                    for (;;) {
+                        double in = dpp_from_left_or(out, wave_in);
+                        if (first || !has_left) in = INFINITY;
+                        bool ch = false;
+                        if (active && in != in_prev) {
+                            in_prev = in;
+                            double cur = vstart[0];
+                            if (has_left) cur = smin(vstart[0], in);     // v[i+1] = min(v[i+1], vf)
+                            bool go = first || !same_bits(cur, v[0]);
+                            v[0] = cur;
 #pragma unroll
-                        for (int k = 0; k + 1 < K; ++k) {
-                            if (!__any(go)) break;
-                            if (go) {
-                                const double vf = vstep_fwd(vc, v[k], ka[k]);
-                                const double nv = (k + 1 < cnt) ? smin(vstart[k + 1], vf) : INFINITY;
-                                go = (it == 0) || !same_bits(nv, v[k + 1]);
-                                v[k + 1] = nv;
+                            for (int k = 0; k + 1 < K; ++k) {
+                                if (!__any(go)) break;
+                                if (go) {
+                                    const double vf = vstep_fwd(vc, v[k], ka[k]);
+                                    const double nv = (k + 1 < cnt) ? smin(vstart[k + 1], vf) : INFINITY;
+                                    go = first || !same_bits(nv, v[k + 1]);
+                                    v[k + 1] = nv;
+                                }
                             }
-                        }
-                        if (has_right) {
-                            if (go) {
+                            if (has_right && go) {
                                 const double o = vstep_fwd(vc, v[K - 1], ka[K - 1]);
-                                changed = (it > 0) && (o != out);
+                                ch = o != out;
                                 out = o;
                             }
-                            sm.u.vin[it & 1][tid] = out;
                         }
-                    } else if (active && has_right) {
-                        sm.u.vin[it & 1][tid] = out;
+                        if (first) { first = false; continue; }
+                        if (!__any(ch)) break;
                     }
-                    if (!__syncthreads_or(changed) && it > 0) break;
+                    if constexpr (NW == 1) break;
+                    bool pch = false;
+                    if (lane == 63 && has_right) {
+                        pch = out != pub;
+                        pub = out;
+                        sm.u.vin[ro & 1][wid] = out;
+                    }
+                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (wid > 0) wave_in = sm.u.vin[ro & 1][wid - 1];
                 }
             }
             // closed wrap (ref:834-839): v[0] = min(v[0], f(v[N-1], k[N-1]))
@@ -611,45 +625,55 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 if (tid == 0) v[0] = smin(v[0], sm.bc[0]);
                 __syncthreads();
             }
-            // ---- backward pass (ref:841-845), with the same early stop
+            // ---- backward pass (ref:841-845): the same relaxation from the right
             {
                 double vpre[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) vpre[k] = v[k];
                 double in_prev = -1.0;
-                double out = 0.0;
-                for (int it = 0;; ++it) {
-                    double in = INFINITY;
-                    if (it > 0 && has_right) in = sm.u.vin[(it - 1) & 1][tid + 1];
-                    bool changed = false;
-                    if (active && in != in_prev) {
-                        in_prev = in;
-                        // has_right => full chunk (only the last thread can be partial)
-                        const double cur = has_right ? smin(vpre[K - 1], in) : vpre[K - 1];
-                        bool go = (it == 0) || !same_bits(cur, v[K - 1]);
-                        v[K - 1] = cur;
+                double out = INFINITY;
+                double wave_in = INFINITY;   // lane 63: the next wave's first outgoing value
+                double pub = -1.0;           // lane 0: the value last published for the previous wave
+                bool first = true;
+                for (int ro = 0;; ++ro) {
+                    for (;;) {
+                        double in = dpp_from_right_or(out, wave_in);
+                        if (first || !has_right) in = INFINITY;
+                        bool ch = false;
+                        if (active && in != in_prev) {
+                            in_prev = in;
+                            // has_right => full chunk (only the last thread can be partial)
+                            const double cur = has_right ? smin(vpre[K - 1], in) : vpre[K - 1];
+                            bool go = first || !same_bits(cur, v[K - 1]);
+                            v[K - 1] = cur;
 #pragma unroll
-                        for (int k = K - 2; k >= 0; --k) {
-                            if (!__any(go)) break;
-                            if (go) {
-                                const double vb = vstep_bwd(vc, v[k + 1], ka[k + 1]);
-                                const double nv = (k < cnt) ? smin(vpre[k], vb) : INFINITY;
-                                go = (it == 0) || !same_bits(nv, v[k]);
-                                v[k] = nv;
+                            for (int k = K - 2; k >= 0; --k) {
+                                if (!__any(go)) break;
+                                if (go) {
+                                    const double vb = vstep_bwd(vc, v[k + 1], ka[k + 1]);
+                                    const double nv = (k < cnt) ? smin(vpre[k], vb) : INFINITY;
+                                    go = first || !same_bits(nv, v[k]);
+                                    v[k] = nv;
+                                }
                             }
-                        }
-                        if (has_left) {
-                            if (go) {
+                            if (has_left && go) {
                                 const double o = vstep_bwd(vc, v[0], ka[0]);
-                                changed = (it > 0) && (o != out);
+                                ch = o != out;
                                 out = o;
                             }
-                            sm.u.vin[it & 1][tid] = out;
                         }
-                    } else if (active && has_left) {
-                        sm.u.vin[it & 1][tid] = out;
+                        if (first) { first = false; continue; }
+                        if (!__any(ch)) break;
                     }
-                    if (!__syncthreads_or(changed) && it > 0) break;
+                    if constexpr (NW == 1) break;
+                    bool pch = false;
+                    if (lane == 0 && has_left) {
+                        pch = out != pub;
+                        pub = out;
+                        sm.u.vin[ro & 1][wid] = out;
+                    }
+                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (wid + 1 < NW) wave_in = sm.u.vin[ro & 1][wid + 1];
                 }
             }
             // closed wrap (ref:846-850): v[N-1] = min(v[N-1], b(v[0], k[0]))

@@ -45,6 +45,18 @@ __device__ __forceinline__ double dpp_s(double x) {
     hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
+// lane l <- lane l-1 (wave_shr:1), lane 0 keeps `edge`; lane l <- lane l+1 (wave_shl:1),
+// lane 63 keeps `edge` (bound_ctrl off: the edge lane is not written)
+__device__ __forceinline__ double dpp_left_or(double x, double edge) {
+    int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x138, 0xf, 0xf, false);
+    int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_right_or(double x, double edge) {
+    int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x130, 0xf, 0xf, false);
+    int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double readlane_s(double x, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
                             __builtin_amdgcn_readlane(__double2loint(x), l));
@@ -273,26 +285,44 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             ++sweeps;
             for (int i = r0; i < r1; ++i) VS[i] = V[i];           // sweep start
             __syncthreads();
-            // forward (ref:829-833)
-            double in_prev = -1.0;
-            for (int it = 0;; ++it) {
-                double in = INFINITY;
-                if (it > 0 && has_left) in = sm.vin[(it - 1) & 1][tid - 1];
-                bool changed = false;
-                if (ract && in != in_prev) {
-                    changed = (it > 0);
-                    in_prev = in;
-                    double cur = has_left ? smin(VS[r0], in) : VS[r0];
-                    V[r0] = cur;
-                    for (int i = r0; i + 1 < r1; ++i) {
-                        cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
-                        V[i + 1] = cur;
+            // forward (ref:829-833): exact chunked relaxation as in rl_kernels.hip -- every
+            // range first evaluates with no incoming constraint, then within a wave a lane
+            // takes its left neighbour's outgoing value by DPP and re-evaluates while it
+            // changes (no barrier); one barrier per round passes the wave edges on
+            {
+                double in_prev = -1.0, out = INFINITY, wave_in = INFINITY, pub = -1.0;
+                bool first = true;
+                for (int ro = 0;; ++ro) {
+                    for (;;) {
+                        double in = dpp_left_or(out, wave_in);
+                        if (first || !has_left) in = INFINITY;
+                        bool ch = false;
+                        if (ract && in != in_prev) {
+                            in_prev = in;
+                            double cur = has_left ? smin(VS[r0], in) : VS[r0];
+                            V[r0] = cur;
+                            for (int i = r0; i + 1 < r1; ++i) {
+                                cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
+                                V[i + 1] = cur;
+                            }
+                            if (has_right) {
+                                const double o = vstep_fwd(vc, cur, KA[r1 - 1]);
+                                ch = o != out;
+                                out = o;
+                            }
+                        }
+                        if (first) { first = false; continue; }
+                        if (!__any(ch)) break;
                     }
-                    if (has_right) sm.vin[it & 1][tid] = vstep_fwd(vc, cur, KA[r1 - 1]);
-                } else if (has_right) {
-                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
+                    bool pch = false;
+                    if (lane == 63 && has_right) {
+                        pch = out != pub;
+                        pub = out;
+                        sm.vin[ro & 1][wid] = out;
+                    }
+                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (wid > 0) wave_in = sm.vin[ro & 1][wid - 1];
                 }
-                if (!__syncthreads_or(changed) && it > 0) break;
             }
             if (CLOSED) {                                          // ref:834-839
                 if (ract && r1 == N) sm.bc[0] = vstep_fwd(vc, V[N - 1], KA[N - 1]);
@@ -303,25 +333,40 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             // backward (ref:841-845)
             for (int i = r0; i < r1; ++i) Q1[i] = V[i];            // pass start (Q1 is free here)
             __syncthreads();
-            in_prev = -1.0;
-            for (int it = 0;; ++it) {
-                double in = INFINITY;
-                if (it > 0 && has_right) in = sm.vin[(it - 1) & 1][tid + 1];
-                bool changed = false;
-                if (ract && in != in_prev) {
-                    changed = (it > 0);
-                    in_prev = in;
-                    double cur = has_right ? smin(Q1[r1 - 1], in) : Q1[r1 - 1];
-                    V[r1 - 1] = cur;
-                    for (int i = r1 - 2; i >= r0; --i) {
-                        cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
-                        V[i] = cur;
+            {
+                double in_prev = -1.0, out = INFINITY, wave_in = INFINITY, pub = -1.0;
+                bool first = true;
+                for (int ro = 0;; ++ro) {
+                    for (;;) {
+                        double in = dpp_right_or(out, wave_in);
+                        if (first || !has_right) in = INFINITY;
+                        bool ch = false;
+                        if (ract && in != in_prev) {
+                            in_prev = in;
+                            double cur = has_right ? smin(Q1[r1 - 1], in) : Q1[r1 - 1];
+                            V[r1 - 1] = cur;
+                            for (int i = r1 - 2; i >= r0; --i) {
+                                cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
+                                V[i] = cur;
+                            }
+                            if (has_left) {
+                                const double o = vstep_bwd(vc, cur, KA[r0]);
+                                ch = o != out;
+                                out = o;
+                            }
+                        }
+                        if (first) { first = false; continue; }
+                        if (!__any(ch)) break;
                     }
-                    if (has_left) sm.vin[it & 1][tid] = vstep_bwd(vc, cur, KA[r0]);
-                } else if (has_left) {
-                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
+                    bool pch = false;
+                    if (lane == 0 && has_left) {
+                        pch = out != pub;
+                        pub = out;
+                        sm.vin[ro & 1][wid] = out;
+                    }
+                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (wid + 1 < NWS) wave_in = sm.vin[ro & 1][wid + 1];
                 }
-                if (!__syncthreads_or(changed) && it > 0) break;
             }
             if (CLOSED) {                                          // ref:846-850
                 if (tid == 0) sm.bc[1] = vstep_bwd(vc, V[0], KA[0]);

@@ -10,6 +10,7 @@ for s in $steps; do
     bench)  specs+=("bench:600:python bench.py > $out/bench.json") ;;
     benchq) specs+=("benchq:300:python bench.py --no-cpu > $out/bench.json") ;;
     stamps) specs+=("stamps:200:python scripts/stamps.py && python scripts/stamps_c5.py") ;;
+    ab)     specs+=("ab:400:python scripts/ab_variants.py 5 > $out/ab.log") ;;
   esac
 done
 bash scripts/gpu_run.sh "$out" "${specs[@]}"
