@@ -185,7 +185,9 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
  * For repeated runs with inputs already resident in HBM (bench, services).
  * create: allocates device buffers on `device` and uploads the inputs.
  * run:    enqueues the optimisation on `hip_stream` (a hipStream_t; NULL = the
- *         plan's own stream) and returns immediately.
+ *         plan's own stream) and returns immediately.  With both modes, the
+ *         min-time kernel runs on a second plan-owned stream, concurrently with the
+ *         min-curvature kernel; `hip_stream` waits for both.
  * fetch:  copies results to host (synchronises the stream used by run).
  * device_outputs: device pointers of the result arrays (for collectives).       */
 typedef struct rl_plan rl_plan;

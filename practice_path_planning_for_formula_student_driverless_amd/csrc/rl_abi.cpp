@@ -183,7 +183,11 @@ struct rl_plan {
     double L = 0, veh_width = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t last_stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // both modes in one run: the min-time kernel runs on aux_stream, concurrently with the
+    // min-curvature kernel (the optimisers are independent); the run stream waits for it
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // run start, mode starts, run end
+    hipEvent_t ev_end[2] = {nullptr, nullptr};                 // mode ends
     bool ran = false;
     double* d_center = nullptr;
     double* d_Ls = nullptr;           // per-instance L (lap evaluation) or nullptr
@@ -305,9 +309,13 @@ int rl_plan_destroy(rl_plan* plan) {
     hipSetDevice(plan->device);
     if (plan->last_stream) hipStreamSynchronize(plan->last_stream);
     for (void* p : plan->allocs) hipFree(p);
+    if (plan->aux_stream) hipStreamSynchronize(plan->aux_stream);
     for (auto& e : plan->ev)
         if (e) hipEventDestroy(e);
+    for (auto& e : plan->ev_end)
+        if (e) hipEventDestroy(e);
     if (plan->own_stream) hipStreamDestroy(plan->own_stream);
+    if (plan->aux_stream) hipStreamDestroy(plan->aux_stream);
     delete plan;
     return RL_OK;
 }
@@ -375,9 +383,12 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
         rl_plan_destroy(p);
         return code;
     };
-    if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(RL_EHIP, "hipStreamCreate failed"));
     for (auto& e : p->ev)
+        if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
+    for (auto& e : p->ev_end)
         if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
 
     const size_t N = (size_t)std::max(p->N, 1);
@@ -455,8 +466,12 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : p->own_stream;
     p->last_stream = st;
     HIPCHK(hipEventRecord(p->ev[0], st));
+    const bool both = (p->modes & (RL_MODE_MINCURV | RL_MODE_MINTIME)) == (RL_MODE_MINCURV | RL_MODE_MINTIME);
+    if (both) HIPCHK(hipStreamWaitEvent(p->aux_stream, p->ev[0], 0));   // everything queued before the run
     for (int m = 0; m < 2; ++m) {
         if (!(p->modes & (1 << m))) continue;
+        hipStream_t st_run = st;
+        st = (both && m == 1) ? p->aux_stream : st_run;
         ModeBufs& mb = p->mb[m];
         const size_t BN = (size_t)p->B * (size_t)std::max(p->N, 1);
         if (p->N == 0 || p->max_outer == 0) {
@@ -468,9 +483,11 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
                 HIPCHK(hipMemsetAsync(mb.sweeps, 0, sizeof(int32_t) * p->B * (p->max_outer + 1), st));
             }
             if (p->N == 0) {
-                // no kernel: record the mode's event anyway, so rl_plan_kernel_ms(1 + m)
+                // no kernel: record the mode's events anyway, so rl_plan_kernel_ms(1 + m)
                 // reports the (empty) interval instead of failing on an unrecorded event
                 HIPCHK(hipEventRecord(p->ev[1 + m], st));
+                HIPCHK(hipEventRecord(p->ev_end[m], st));
+                st = st_run;
                 continue;
             }
         }
@@ -500,7 +517,10 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         HIPCHK(hipEventRecord(p->ev[1 + m], st));
         hipError_t e = p->stream ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
+        HIPCHK(hipEventRecord(p->ev_end[m], st));
+        st = st_run;
     }
+    if (both) HIPCHK(hipStreamWaitEvent(st, p->ev_end[1], 0));
     HIPCHK(hipEventRecord(p->ev[3], st));
     p->ran = true;
     return RL_OK;
@@ -759,8 +779,8 @@ int rl_plan_kernel_ms(rl_plan* p, int32_t idx, float* ms) {
     hipEvent_t a, b;
     const bool mc = p->modes & RL_MODE_MINCURV, mt = p->modes & RL_MODE_MINTIME;
     if (idx == 0) { a = p->ev[0]; b = p->ev[3]; }
-    else if (idx == 1 && mc) { a = p->ev[1]; b = mt ? p->ev[2] : p->ev[3]; }
-    else if (idx == 2 && mt) { a = p->ev[2]; b = p->ev[3]; }
+    else if (idx == 1 && mc) { a = p->ev[1]; b = p->ev_end[0]; }
+    else if (idx == 2 && mt) { a = p->ev[2]; b = p->ev_end[1]; }
     else return fail(RL_EINVAL, "kernel index not in this plan");
     HIPCHK(hipEventElapsedTime(ms, a, b));
     return RL_OK;
