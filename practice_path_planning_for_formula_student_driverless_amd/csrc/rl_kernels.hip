@@ -43,6 +43,9 @@ constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per
 #ifndef RL_MD_TIGHT
 #define RL_MD_TIGHT 0    // fallback search: nearest-midpoint radius pass (rl_corridor.h ring_mindist; A/B: +0.8% C2 here, -21% C5 in the streaming kernel)
 #endif
+#ifndef RL_VP_ROUNDS
+#define RL_VP_ROUNDS 8   // v-pass: in-wave relaxation rounds between two cross-wave exchanges (barriers)
+#endif
 #ifndef RL_MD_PRUNE
 #define RL_MD_PRUNE 1    // fallback search: running-minimum pruning in the exact walk
 #endif
@@ -574,7 +577,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 double pub = -1.0;           // lane 63: the value last published for the next wave
                 bool first = true;
                 for (int ro = 0;; ++ro) {
-                    for (;;) {
+                    bool conv = false;         // wave-uniform: the in-wave relaxation settled
+                    for (int ir = 0; ir < ((NW == 1) ? 0x7fffffff : RL_VP_ROUNDS); ++ir) {
                         double in = dpp_from_left_or(out, wave_in);
                         if (first || !has_left) in = INFINITY;
                         bool ch = false;
@@ -601,7 +605,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                             }
                         }
                         if (first) { first = false; continue; }
-                        if (!__any(ch)) break;
+                        if (!__any(ch)) { conv = true; break; }
                     }
                     if constexpr (NW == 1) break;
                     bool pch = false;
@@ -610,7 +614,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                         pub = out;
                         sm.u.vin[ro & 1][wid] = out;
                     }
-                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid > 0) wave_in = sm.u.vin[ro & 1][wid - 1];
                 }
             }
@@ -636,7 +640,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 double pub = -1.0;           // lane 0: the value last published for the previous wave
                 bool first = true;
                 for (int ro = 0;; ++ro) {
-                    for (;;) {
+                    bool conv = false;         // wave-uniform: the in-wave relaxation settled
+                    for (int ir = 0; ir < ((NW == 1) ? 0x7fffffff : RL_VP_ROUNDS); ++ir) {
                         double in = dpp_from_right_or(out, wave_in);
                         if (first || !has_right) in = INFINITY;
                         bool ch = false;
@@ -663,7 +668,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                             }
                         }
                         if (first) { first = false; continue; }
-                        if (!__any(ch)) break;
+                        if (!__any(ch)) { conv = true; break; }
                     }
                     if constexpr (NW == 1) break;
                     bool pch = false;
@@ -672,7 +677,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                         pub = out;
                         sm.u.vin[ro & 1][wid] = out;
                     }
-                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid + 1 < NW) wave_in = sm.u.vin[ro & 1][wid + 1];
                 }
             }

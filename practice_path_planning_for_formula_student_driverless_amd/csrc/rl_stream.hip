@@ -76,6 +76,9 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 #ifndef RL_SCK
 #define RL_SCK 2
 #endif
+#ifndef RL_VP_ROUNDS
+#define RL_VP_ROUNDS 8   // v-pass: in-wave relaxation rounds between two cross-wave exchanges (barriers)
+#endif
 #ifndef RL_BT_BATCH
 #define RL_BT_BATCH 4
 #endif
@@ -293,7 +296,8 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 double in_prev = -1.0, out = INFINITY, wave_in = INFINITY, pub = -1.0;
                 bool first = true;
                 for (int ro = 0;; ++ro) {
-                    for (;;) {
+                    bool conv = false;         // wave-uniform: the in-wave relaxation settled
+                    for (int ir = 0; ir < RL_VP_ROUNDS; ++ir) {
                         double in = dpp_left_or(out, wave_in);
                         if (first || !has_left) in = INFINITY;
                         bool ch = false;
@@ -312,7 +316,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                             }
                         }
                         if (first) { first = false; continue; }
-                        if (!__any(ch)) break;
+                        if (!__any(ch)) { conv = true; break; }
                     }
                     bool pch = false;
                     if (lane == 63 && has_right) {
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         pub = out;
                         sm.vin[ro & 1][wid] = out;
                     }
-                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid > 0) wave_in = sm.vin[ro & 1][wid - 1];
                 }
             }
@@ -337,7 +341,8 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 double in_prev = -1.0, out = INFINITY, wave_in = INFINITY, pub = -1.0;
                 bool first = true;
                 for (int ro = 0;; ++ro) {
-                    for (;;) {
+                    bool conv = false;         // wave-uniform: the in-wave relaxation settled
+                    for (int ir = 0; ir < RL_VP_ROUNDS; ++ir) {
                         double in = dpp_right_or(out, wave_in);
                         if (first || !has_right) in = INFINITY;
                         bool ch = false;
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                             }
                         }
                         if (first) { first = false; continue; }
-                        if (!__any(ch)) break;
+                        if (!__any(ch)) { conv = true; break; }
                     }
                     bool pch = false;
                     if (lane == 0 && has_left) {
@@ -364,7 +369,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         pub = out;
                         sm.vin[ro & 1][wid] = out;
                     }
-                    if (!__syncthreads_or(pch) && ro > 0) break;
+                    if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid + 1 < NWS) wave_in = sm.vin[ro & 1][wid + 1];
                 }
             }

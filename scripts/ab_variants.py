@@ -35,7 +35,7 @@ def fetch(lib, h, B, N, mo, mt):
 res = {}
 CASES = [("C2", "cmap1_n2000", 1024, 1, 1, False), ("C3mt", "cmap1_n2000_vp20", 256, 2, 2, True),
          ("C3big", "cmap1_n2000_vp20", 4096, 2, 2, True), ("C5", "oval_n10000", 1024, 1, 1, False),
-         ("C5mt", "oval_n10000", 1024, 2, 2, True)]
+         ("C5mt", "oval_n10000", 1024, 2, 2, True), ("C4t3", "track_competition_map_testday3", 512, 3, 0, True)]
 sel = os.environ.get("AB_CASES")
 for cname, cfgname, B, modes, idx, mt in [c for c in CASES if not sel or c[0] in sel.split(",")]:
     case = O.load_case(cfgname); prob = O.case_problem(case); cfg = O.case_cfg(case)
