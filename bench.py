@@ -32,6 +32,12 @@ import time
 
 import numpy as np
 
+# HIP hardware queues for this process (HIP's default is 4): the C4 line runs 7 plans with
+# both modes concurrently (14 streams); with 4 queues the streams share queues and serialise
+# (C4 23.3 ms), with 16 they run side by side (18.4 ms; scripts/c4_sched.py).  Read by the
+# HIP runtime at initialisation, so it is set before anything touches HIP.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))

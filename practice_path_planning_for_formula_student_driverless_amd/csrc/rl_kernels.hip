@@ -43,9 +43,19 @@ constexpr int CK = (RL_CK < 8 ? RL_CK : 8);   // corridor sub-chunk (samples per
 #ifndef RL_MD_TIGHT
 #define RL_MD_TIGHT 0    // fallback search: nearest-midpoint radius pass (rl_corridor.h ring_mindist; A/B: +0.8% C2 here, -21% C5 in the streaming kernel)
 #endif
+// v-pass: in-wave relaxation rounds between two cross-wave exchanges (barriers), per shape.
+// A/B (scripts/ab_variants.py, caps 1 (= one barrier per round), 2, 4, 8, 16): the (4, 512)
+// latency shape gains 5 % from 8-16 rounds; the (8, 256) throughput shape at two instances
+// per CU loses 1-3 % with any cap above 1 (a chain that reaches a wave edge waits for the
+// slowest wave's rounds), so it keeps one barrier per round; single-wave instances need
+// no barrier at all.
 #ifndef RL_VP_ROUNDS
-#define RL_VP_ROUNDS 8   // v-pass: in-wave relaxation rounds between two cross-wave exchanges (barriers)
+#define RL_VP_ROUNDS 16
 #endif
+template <int K, int T>
+struct VpRounds {
+    static constexpr int value = (T == 64) ? 0x7fffffff : ((K == 4 && T == 512) ? RL_VP_ROUNDS : 1);
+};
 #ifndef RL_MD_PRUNE
 #define RL_MD_PRUNE 1    // fallback search: running-minimum pruning in the exact walk
 #endif
@@ -578,7 +588,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 bool first = true;
                 for (int ro = 0;; ++ro) {
                     bool conv = false;         // wave-uniform: the in-wave relaxation settled
-                    for (int ir = 0; ir < ((NW == 1) ? 0x7fffffff : RL_VP_ROUNDS); ++ir) {
+                    for (int ir = 0; ir < VpRounds<K, T>::value; ++ir) {
                         double in = dpp_from_left_or(out, wave_in);
                         if (first || !has_left) in = INFINITY;
                         bool ch = false;
@@ -641,7 +651,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 bool first = true;
                 for (int ro = 0;; ++ro) {
                     bool conv = false;         // wave-uniform: the in-wave relaxation settled
-                    for (int ir = 0; ir < ((NW == 1) ? 0x7fffffff : RL_VP_ROUNDS); ++ir) {
+                    for (int ir = 0; ir < VpRounds<K, T>::value; ++ir) {
                         double in = dpp_from_right_or(out, wave_in);
                         if (first || !has_right) in = INFINITY;
                         bool ch = false;

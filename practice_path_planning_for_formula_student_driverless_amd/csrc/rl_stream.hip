@@ -45,18 +45,6 @@ __device__ __forceinline__ double dpp_s(double x) {
     hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
-// lane l <- lane l-1 (wave_shr:1), lane 0 keeps `edge`; lane l <- lane l+1 (wave_shl:1),
-// lane 63 keeps `edge` (bound_ctrl off: the edge lane is not written)
-__device__ __forceinline__ double dpp_left_or(double x, double edge) {
-    int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x138, 0xf, 0xf, false);
-    int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x138, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double dpp_right_or(double x, double edge) {
-    int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x130, 0xf, 0xf, false);
-    int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x130, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
 __device__ __forceinline__ double readlane_s(double x, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
                             __builtin_amdgcn_readlane(__double2loint(x), l));
@@ -75,9 +63,6 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 // 4 -> 41.6 ms; scripts/ab_c5.py)
 #ifndef RL_SCK
 #define RL_SCK 2
-#endif
-#ifndef RL_VP_ROUNDS
-#define RL_VP_ROUNDS 8   // v-pass: in-wave relaxation rounds between two cross-wave exchanges (barriers)
 #endif
 #ifndef RL_BT_BATCH
 #define RL_BT_BATCH 4
@@ -277,6 +262,8 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     const int r0 = min(N, tid * Cr), r1 = min(N, r0 + Cr);
     const bool ract = r0 < r1;
     const bool has_left = ract && r0 > 0, has_right = ract && r1 < N;
+    // (A/B, round 3: the register kernel's in-wave DPP relaxation made this kernel's C5
+    // min-time run 5-15 % slower at every round cap tried -- one barrier per round stays)
     auto vpass = [&]() -> int {
         const VConst vc = sm.vc;
         for (int i = r0; i < r1; ++i) {
@@ -288,45 +275,26 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             ++sweeps;
             for (int i = r0; i < r1; ++i) VS[i] = V[i];           // sweep start
             __syncthreads();
-            // forward (ref:829-833): exact chunked relaxation as in rl_kernels.hip -- every
-            // range first evaluates with no incoming constraint, then within a wave a lane
-            // takes its left neighbour's outgoing value by DPP and re-evaluates while it
-            // changes (no barrier); one barrier per round passes the wave edges on
-            {
-                double in_prev = -1.0, out = INFINITY, wave_in = INFINITY, pub = -1.0;
-                bool first = true;
-                for (int ro = 0;; ++ro) {
-                    bool conv = false;         // wave-uniform: the in-wave relaxation settled
-                    for (int ir = 0; ir < RL_VP_ROUNDS; ++ir) {
-                        double in = dpp_left_or(out, wave_in);
-                        if (first || !has_left) in = INFINITY;
-                        bool ch = false;
-                        if (ract && in != in_prev) {
-                            in_prev = in;
-                            double cur = has_left ? smin(VS[r0], in) : VS[r0];
-                            V[r0] = cur;
-                            for (int i = r0; i + 1 < r1; ++i) {
-                                cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
-                                V[i + 1] = cur;
-                            }
-                            if (has_right) {
-                                const double o = vstep_fwd(vc, cur, KA[r1 - 1]);
-                                ch = o != out;
-                                out = o;
-                            }
-                        }
-                        if (first) { first = false; continue; }
-                        if (!__any(ch)) { conv = true; break; }
+            // forward (ref:829-833)
+            double in_prev = -1.0;
+            for (int it = 0;; ++it) {
+                double in = INFINITY;
+                if (it > 0 && has_left) in = sm.vin[(it - 1) & 1][tid - 1];
+                bool changed = false;
+                if (ract && in != in_prev) {
+                    changed = (it > 0);
+                    in_prev = in;
+                    double cur = has_left ? smin(VS[r0], in) : VS[r0];
+                    V[r0] = cur;
+                    for (int i = r0; i + 1 < r1; ++i) {
+                        cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
+                        V[i + 1] = cur;
                     }
-                    bool pch = false;
-                    if (lane == 63 && has_right) {
-                        pch = out != pub;
-                        pub = out;
-                        sm.vin[ro & 1][wid] = out;
-                    }
-                    if (!__syncthreads_or(pch || !conv) && ro > 0) break;
-                    if (wid > 0) wave_in = sm.vin[ro & 1][wid - 1];
+                    if (has_right) sm.vin[it & 1][tid] = vstep_fwd(vc, cur, KA[r1 - 1]);
+                } else if (has_right) {
+                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
                 }
+                if (!__syncthreads_or(changed) && it > 0) break;
             }
             if (CLOSED) {                                          // ref:834-839
                 if (ract && r1 == N) sm.bc[0] = vstep_fwd(vc, V[N - 1], KA[N - 1]);
@@ -337,41 +305,25 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             // backward (ref:841-845)
             for (int i = r0; i < r1; ++i) Q1[i] = V[i];            // pass start (Q1 is free here)
             __syncthreads();
-            {
-                double in_prev = -1.0, out = INFINITY, wave_in = INFINITY, pub = -1.0;
-                bool first = true;
-                for (int ro = 0;; ++ro) {
-                    bool conv = false;         // wave-uniform: the in-wave relaxation settled
-                    for (int ir = 0; ir < RL_VP_ROUNDS; ++ir) {
-                        double in = dpp_right_or(out, wave_in);
-                        if (first || !has_right) in = INFINITY;
-                        bool ch = false;
-                        if (ract && in != in_prev) {
-                            in_prev = in;
-                            double cur = has_right ? smin(Q1[r1 - 1], in) : Q1[r1 - 1];
-                            V[r1 - 1] = cur;
-                            for (int i = r1 - 2; i >= r0; --i) {
-                                cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
-                                V[i] = cur;
-                            }
-                            if (has_left) {
-                                const double o = vstep_bwd(vc, cur, KA[r0]);
-                                ch = o != out;
-                                out = o;
-                            }
-                        }
-                        if (first) { first = false; continue; }
-                        if (!__any(ch)) { conv = true; break; }
+            in_prev = -1.0;
+            for (int it = 0;; ++it) {
+                double in = INFINITY;
+                if (it > 0 && has_right) in = sm.vin[(it - 1) & 1][tid + 1];
+                bool changed = false;
+                if (ract && in != in_prev) {
+                    changed = (it > 0);
+                    in_prev = in;
+                    double cur = has_right ? smin(Q1[r1 - 1], in) : Q1[r1 - 1];
+                    V[r1 - 1] = cur;
+                    for (int i = r1 - 2; i >= r0; --i) {
+                        cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
+                        V[i] = cur;
                     }
-                    bool pch = false;
-                    if (lane == 0 && has_left) {
-                        pch = out != pub;
-                        pub = out;
-                        sm.vin[ro & 1][wid] = out;
-                    }
-                    if (!__syncthreads_or(pch || !conv) && ro > 0) break;
-                    if (wid + 1 < NWS) wave_in = sm.vin[ro & 1][wid + 1];
+                    if (has_left) sm.vin[it & 1][tid] = vstep_bwd(vc, cur, KA[r0]);
+                } else if (has_left) {
+                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
                 }
+                if (!__syncthreads_or(changed) && it > 0) break;
             }
             if (CLOSED) {                                          // ref:846-850
                 if (tid == 0) sm.bc[1] = vstep_bwd(vc, V[0], KA[0]);
