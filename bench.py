@@ -36,7 +36,7 @@ import numpy as np
 # both modes concurrently (14 streams); with 4 queues the streams share queues and serialise
 # (C4 23.3 ms), with 16 they run side by side (18.4 ms; scripts/c4_sched.py).  Read by the
 # HIP runtime at initialisation, so it is set before anything touches HIP.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+os.environ["GPU_MAX_HW_QUEUES"] = "16"     # the box exports 4 (HIP's default); <= 32 is allowed
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)

@@ -185,7 +185,8 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
  * For repeated runs with inputs already resident in HBM (bench, services).
  * create: allocates device buffers on `device` and uploads the inputs.
  * run:    enqueues the optimisation on `hip_stream` (a hipStream_t; NULL = the
- *         plan's own stream) and returns immediately.  With both modes, the
+ *         plan's own stream) and returns immediately.  With both modes and a batch
+ *         that leaves the GPU partly idle (B x waves per instance <= 8 x CUs), the
  *         min-time kernel runs on a second plan-owned stream, concurrently with the
  *         min-curvature kernel; `hip_stream` waits for both.
  * fetch:  copies results to host (synchronises the stream used by run).

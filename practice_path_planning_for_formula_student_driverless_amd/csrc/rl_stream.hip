@@ -64,6 +64,9 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 #ifndef RL_SCK
 #define RL_SCK 2
 #endif
+#ifndef RL_BT_FIRST
+#define RL_BT_FIRST 1    // the first trial of an inner iteration joins a batch (its vectors stored)
+#endif
 #ifndef RL_BT_BATCH
 #define RL_BT_BATCH 4
 #endif
@@ -563,7 +566,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         // block_sum_s reduces each sum on its own, so J and the decrease of every step
         // are bit-identical to one-at-a-time trials.  Writes nothing.
         constexpr int MB = RL_BT_BATCH;
-        auto eval_trials = [&](const double (&st)[MB], int m, double (&Jn)[MB], double (&dn)[MB]) {
+        // keep0: step 0 is the first trial of an inner iteration -- also store its α_trial,
+        // q1, q2 and D1α (eval_trial's `keep`), so an accepted first step needs no second pass
+        auto eval_trials = [&](const double (&st)[MB], int m, double (&Jn)[MB], double (&dn)[MB], bool keep0) {
             double s3[3 * MB];
 #pragma unroll
             for (int j = 0; j < 3 * MB; ++j) s3[j] = 0.0;
@@ -582,6 +587,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         const double ap = (ip == i) ? a0 : smin(hip, smax(lop, apv - st[j] * gp));
                         const double x1 = d1_at(i, am, a0, ap), x2 = d2_at(i, am, a0, ap);
                         const double r = w * (n0 + A1 * x1 + A2 * x2);
+                        if (j == 0 && keep0) {                         // term_at's q1, q2 (ref:667)
+                            const double Wz = MT ? w * g2 * r : w * r;
+                            an_p[i] = a0; Q1[i] = A1 * Wz; Q2[i] = A2 * Wz; D1[i] = x1;
+                        }
                         s3[3 * j] += MT ? g2 * r * r : r * r;        // term_at's jz (ref:881 / 661)
                         s3[3 * j + 1] += x1 * x1;
                         s3[3 * j + 2] += g0 * (a0 - a0v);
@@ -603,7 +612,8 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
-                if (MB > 1 && bt > 0) {
+                if (MB > 1 && (RL_BT_FIRST || bt > 0)) {
+                    const bool kept = bt == 0;             // step 0's vectors are stored by the pass
                     // the steps ref:737-740 would try next: halve, stop at 20 backtracks
                     // or below step_min
                     double st[MB], Jn[MB], dn[MB];
@@ -615,12 +625,12 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         st[j] = sj;
                         if (m == j && bt + j < 20 && !(sj < C.step_min)) m = j + 1;
                     }
-                    eval_trials(st, m, Jn, dn);
+                    eval_trials(st, m, Jn, dn, kept);
                     bool stop = false;
                     for (int j = 0; j < m; ++j) {
                         ++evals;
                         if (Jn[j] <= J + C.armijo_c * dn[j]) {
-                            materialize(st[j]);
+                            if (!(kept && j == 0)) materialize(st[j]);
                             double* t = al_p; al_p = an_p; an_p = t;
                             eval_grad();
                             J = Jn[j];
