@@ -612,7 +612,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
-                if (MB > 1 && (RL_BT_FIRST || bt > 0)) {
+                // (the first trial joins a batch for min-curv only: A/B, C5 27.8 -> 26.4 ms;
+                // min-time, with its higher register pressure, 67.2 -> 69.8 ms)
+                if (MB > 1 && ((RL_BT_FIRST && !MT) || bt > 0)) {
                     const bool kept = bt == 0;             // step 0's vectors are stored by the pass
                     // the steps ref:737-740 would try next: halve, stop at 20 backtracks
                     // or below step_min

@@ -16,8 +16,8 @@ for s in $steps; do
     bench)  specs+=("bench:600:python bench.py > $out/bench.json") ;;
     stats)  specs+=("stats:300:rocprofv3 --kernel-trace --stats -d $out/stats -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-extras") ;;
     stats5) specs+=("stats5:300:rocprofv3 --kernel-trace --stats -d $out/stats5 -o run --output-format csv -- python scripts/run_c5.py") ;;
-    pmc2)   specs+=("pmc2:900:bash scripts/pmc.sh $out/pmc2 && python scripts/pmc_summary.py $out/pmc2 --commit --key c2_mincurv --profile profiles/r02/c2_pmc_summary.json") ;;
-    pmc5)   specs+=("pmc5:900:PMC_CMD='python scripts/run_c5.py' bash scripts/pmc.sh $out/pmc5 && python scripts/pmc_summary.py $out/pmc5 --commit --key c5_mincurv --profile profiles/r02/c5_pmc_summary.json") ;;
+    pmc2)   specs+=("pmc2:900:bash scripts/pmc.sh $out/pmc2 && python scripts/pmc_summary.py $out/pmc2 --commit --key c2_mincurv --profile profiles/${RND:-r03}/c2_pmc_summary.json") ;;
+    pmc5)   specs+=("pmc5:900:PMC_CMD='python scripts/run_c5.py' bash scripts/pmc.sh $out/pmc5 && python scripts/pmc_summary.py $out/pmc5 --commit --key c5_mincurv --profile profiles/${RND:-r03}/c5_pmc_summary.json") ;;
   esac
 done
 bash scripts/gpu_run.sh "$out" "${specs[@]}"
