@@ -9,7 +9,7 @@ lib = abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_st
 names = ["setup", "corridor tail (combine, LDS, seed)", "mt:κ/vpass/γ", "lin-geom", "PGD loop", "update", "final",
          "normals + corridor loads", "corridor: inner-ring rays", "corridor: outer-ring rays", "corridor: fallback search",
          "-", "-", "-", "-", "-"]
-for cname, B, modes in (("cmap1_n2000", 1024, 1), ("cmap1_n2000_vp20", 256, 2)):
+for cname, B, modes in (("cmap1_n2000", 1024, 1), ("cmap1_n2000_vp20", 256, 2), ("cmap1_n2000_vp20", 4096, 2)):
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)
     h = C.c_void_p(); p = prob.as_c(); arr, n = abi.cfg_array(cfg)
     seeds = np.arange(B, dtype=np.uint64)

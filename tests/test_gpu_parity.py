@@ -180,9 +180,12 @@ def _synthetic(N, closed, rng):
 
 
 @pytest.mark.parametrize("closed", [True, False])
-@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 1000, 1023, 1025, 2047, 2049])
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 1000, 1023, 1025, 1536, 2047, 2048, 2049,
+                               3072, 4096])
 def test_ragged_sizes_vs_oracle(N, closed):
-    """Every kernel variant (K,T) and every partial-chunk shape, closed and open."""
+    """Every kernel variant (K,T) and every partial-chunk shape, closed and open.  The
+    multiples of K with three or more waves per instance (1536, 2048, 3072, 4096) run the
+    open interior-stencil path in waves that hold no boundary sample."""
     _lib_or_skip()
     rng = np.random.default_rng(N)
     prob = _synthetic(N, closed, rng)
