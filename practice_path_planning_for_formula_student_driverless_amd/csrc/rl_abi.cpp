@@ -60,7 +60,7 @@ struct RingHost {
     std::vector<double> vtx;        // [M][2]
     std::vector<rl::SegRec> rec;    // [M]
     std::vector<uint32_t> flag;     // [M/32]
-    std::vector<double> blk;        // [M/8][4] block circles (rl_corridor.h block culling)
+    std::vector<double> blk;        // [M/B][4] block circles (rl_corridor.h block culling)
     int M = 0, E = 0;
     double dl0 = 0, dl32 = 0;
 };

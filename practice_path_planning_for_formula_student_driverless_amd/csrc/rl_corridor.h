@@ -45,18 +45,28 @@ struct RingDesc {
     const double2* vtx;       // [M] entry vertex (NaN for padding)
     const SegRec* rec;        // [M] record of the segment ending at the entry
     const uint32_t* flag;     // [M/32] bit (31-j): entry 32b+j ends a segment
-    const double* blk;        // ring_blk_doubles(M): [M/8][4] block circles (cx, cy, R, 0), R < 0: no segment
+    const double* blk;        // ring_blk_doubles(M): [M/B][4] block circles (cx, cy, R, 0), R < 0: no segment
                               // ends in the block; then the side filter's fp32 copies: vertices [M][2] f32
-                              // and block circles [M/8][4] f32 (radius rounded up), and the fallback
+                              // and block circles [M/B][4] f32 (radius rounded up), and the fallback
                               // filters' segment midpoints [M][4] f32 (mx, my, half length rounded up, 0)
     int32_t M, E;             // padded entry count, segment count
     double dl0;               // 4e-12*(1+Vmax) + 4e-15*Rv
     double dl32;              // 1e-6*Rv: the fp32 side filter's extra margin (see ring_rays)
 };
-__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return M / 2 + M + M / 4 + 2 * M; }
+#ifndef RL_BLKSZ
+#define RL_BLKSZ 8       // entries per culling block (4 or 8; A/B knob)
+#endif
+constexpr int RL_BLK = RL_BLKSZ;
+static_assert(RL_BLK == 4 || RL_BLK == 8, "culling blocks of 4 or 8 entries");
+// layout of RingDesc::blk: [M/B][4] fp64 circles, then fp32 vertices [M][2], fp32 circles
+// [M/B][4] and fp32 midpoints [M][4] (counted in doubles)
+__host__ __device__ constexpr size_t ring_blk_off_vtx32(size_t M) { return 4 * M / RL_BLK; }
+__host__ __device__ constexpr size_t ring_blk_off_blk32(size_t M) { return 4 * M / RL_BLK + M; }
+__host__ __device__ constexpr size_t ring_blk_off_mid32(size_t M) { return 4 * M / RL_BLK + M + 2 * M / RL_BLK; }
+__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return ring_blk_off_mid32(M) + 2 * M; }
 typedef __attribute__((address_space(4))) const float cflt;
 
-// Block culling. Entries come in blocks of 8. The host gives each block a circle (C, R)
+// Block culling. Entries come in blocks of RL_BLK. The host gives each block a circle (C, R)
 // that contains both endpoints of every segment ending in the block (rl_abi.cpp
 // make_ring), so every point of those segments lies within R of C.
 //  * Ray filter: |n x (V - C)| <= |n| R for every such vertex V. If the centre's side
@@ -66,7 +76,6 @@ typedef __attribute__((address_space(4))) const float cflt;
 //  * Fallback: the distance to any segment of the block is >= |q - C| - R.
 // A block is skipped only when every lane's samples skip it, so the entry loop stays
 // wave-uniform. What survives is exactly what the entry tests would keep.
-constexpr int RL_BLK = 8;
 
 // Diagnostic build only (-DRL_COUNT=1): corridor work counters (lane-level events),
 // summed with atomics into a device array no other code reads.
@@ -123,8 +132,8 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
                                           const double (&ux)[CK], const double (&uy)[CK], const bool (&act)[CK],
                                           double (&bp)[CK], double (&bn)[CK], double (&ub2)[CK]) {
     cu32* F = as_cu32(R.flag);
-    cflt* V = (cflt*)(R.blk + R.M / 2);                  // fp32 vertices [M][2]
-    cflt* BK = (cflt*)(R.blk + R.M / 2 + R.M);           // fp32 block circles [M/8][4]
+    cflt* V = (cflt*)(R.blk + ring_blk_off_vtx32(R.M));     // fp32 vertices [M][2]
+    cflt* BK = (cflt*)(R.blk + ring_blk_off_blk32(R.M));    // fp32 block circles [M/B][4]
     const SegRec* __restrict__ S = R.rec;  // per-lane (divergent) reads
     // The side filter runs in fp32 (packed for two samples per lane).  c = n x (V - P) =
     // ux*vy - uy*vx - g.  With e = 2^-24 and |n| <= 1, the fp32 value built from fp32
@@ -191,7 +200,7 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
                 continue;
             }
             const int e0 = b0 + q * RL_BLK;
-            uint32_t pb[CK], qb[CK];   // bit 8: the entry before the block, bit 7-j: entry e0+j
+            uint32_t pb[CK], qb[CK];   // bit B: the entry before the block, bit B-1-j: entry e0+j
 #pragma unroll
             for (int k = 0; k < CK; ++k) { pb[k] = lp[k]; qb[k] = lq[k]; }
             if (!prev_ok) {
@@ -221,8 +230,9 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
                 // a pair is skipped only when both endpoints lie beyond dl on the same side
-                uint32_t cand = ~((pb[k] & (pb[k] >> 1)) | (qb[k] & (qb[k] >> 1))) & 0xFFu;
-                if (bad[k]) cand = 0xFFu;
+                constexpr uint32_t BM = (1u << RL_BLK) - 1u;
+                uint32_t cand = ~((pb[k] & (pb[k] >> 1)) | (qb[k] & (qb[k] >> 1))) & BM;
+                if (bad[k]) cand = BM;
                 w[k] = (w[k] << RL_BLK) | cand;
                 lp[k] = pb[k] & 1u;
                 lq[k] = qb[k] & 1u;
@@ -273,8 +283,8 @@ template <int CK, bool TIGHT = true, bool PRUNE = true>
 __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
                                              const bool (&need)[CK], const double (&rad)[CK], double (&md)[CK]) {
     cu32* F = as_cu32(R.flag);
-    cflt* BK = (cflt*)(R.blk + R.M / 2 + R.M);            // fp32 block circles [M/8][4]
-    cflt* MD = (cflt*)(R.blk + R.M / 2 + R.M + R.M / 4);   // fp32 (mx, my, hr, 0) [M][4]
+    cflt* BK = (cflt*)(R.blk + ring_blk_off_blk32(R.M));    // fp32 block circles [M/B][4]
+    cflt* MD = (cflt*)(R.blk + ring_blk_off_mid32(R.M));    // fp32 (mx, my, hr, 0) [M][4]
     const SegRec* __restrict__ S = R.rec;
     const double cx = qx[0], cy = qy[0];
     double dk[CK];                         // |q_k - q0|_1, rounded up
