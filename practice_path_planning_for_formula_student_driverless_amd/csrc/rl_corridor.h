@@ -54,10 +54,14 @@ struct RingDesc {
     double dl32;              // 1e-6*Rv: the fp32 side filter's extra margin (see ring_rays)
 };
 #ifndef RL_BLKSZ
-#define RL_BLKSZ 8       // entries per culling block (4 or 8; A/B knob)
+#define RL_BLKSZ 16      // entries per culling block (4, 8, 16 or 32; A/B in DESIGN 3d)
 #endif
 constexpr int RL_BLK = RL_BLKSZ;
-static_assert(RL_BLK == 4 || RL_BLK == 8, "culling blocks of 4 or 8 entries");
+static_assert(RL_BLK == 4 || RL_BLK == 8 || RL_BLK == 16 || RL_BLK == 32, "culling blocks of 4, 8, 16 or 32 entries");
+// the side bits of a visited block are assembled RL_SUB entries at a time (RL_SUB + 1 bits per word)
+constexpr int RL_SUB = RL_BLK < 16 ? RL_BLK : 16;
+// a candidate word shifted past one skipped block
+__device__ __forceinline__ uint32_t shl_blk(uint32_t w) { return RL_BLK >= 32 ? 0u : (w << (RL_BLK & 31)); }
 // layout of RingDesc::blk: [M/B][4] fp64 circles, then fp32 vertices [M][2], fp32 circles
 // [M/B][4] and fp32 midpoints [M][4] (counted in doubles)
 __host__ __device__ constexpr size_t ring_blk_off_vtx32(size_t M) { return 4 * M / RL_BLK; }
@@ -173,7 +177,7 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
         uint32_t w[CK];
 #pragma unroll
         for (int k = 0; k < CK; ++k) w[k] = 0u;
-        // which of the word's 4 blocks some lane's ray line may cross (wave-uniform)
+        // which of the word's 32/RL_BLK blocks some lane's ray line may cross (wave-uniform)
         uint32_t visit = 0u;
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
@@ -195,12 +199,14 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
         for (int q = 0; q < 32 / RL_BLK; ++q) {
             if (!((visit >> q) & 1u)) {
 #pragma unroll
-                for (int k = 0; k < CK; ++k) w[k] <<= RL_BLK;
+                for (int k = 0; k < CK; ++k) w[k] = shl_blk(w[k]);
                 prev_ok = false;
                 continue;
             }
-            const int e0 = b0 + q * RL_BLK;
-            uint32_t pb[CK], qb[CK];   // bit B: the entry before the block, bit B-1-j: entry e0+j
+#pragma unroll
+          for (int sb = 0; sb < RL_BLK / RL_SUB; ++sb) {
+            const int e0 = b0 + q * RL_BLK + sb * RL_SUB;
+            uint32_t pb[CK], qb[CK];   // bit S: the entry before the sub-block, bit S-1-j: entry e0+j
 #pragma unroll
             for (int k = 0; k < CK; ++k) { pb[k] = lp[k]; qb[k] = lq[k]; }
             if (!prev_ok) {
@@ -218,7 +224,7 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
                 }
             }
 #pragma unroll
-            for (int j = 0; j < RL_BLK; ++j) {
+            for (int j = 0; j < RL_SUB; ++j) {
                 const float vx = V[2 * (e0 + j)], vy = V[2 * (e0 + j) + 1];
 #pragma unroll
                 for (int k = 0; k < CK; ++k) {
@@ -230,14 +236,15 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
 #pragma unroll
             for (int k = 0; k < CK; ++k) {
                 // a pair is skipped only when both endpoints lie beyond dl on the same side
-                constexpr uint32_t BM = (1u << RL_BLK) - 1u;
+                constexpr uint32_t BM = (1u << RL_SUB) - 1u;
                 uint32_t cand = ~((pb[k] & (pb[k] >> 1)) | (qb[k] & (qb[k] >> 1))) & BM;
                 if (bad[k]) cand = BM;
-                w[k] = (w[k] << RL_BLK) | cand;
+                w[k] = (RL_SUB >= 32 ? 0u : (w[k] << (RL_SUB & 31))) | cand;
                 lp[k] = pb[k] & 1u;
                 lq[k] = qb[k] & 1u;
             }
             prev_ok = true;
+          }
         }
         const uint32_t f = F[b0 >> 5];
 #pragma unroll
@@ -355,7 +362,7 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
         uint32_t w = 0u;
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
-            if (!((visit >> q) & 1u)) { w <<= RL_BLK; continue; }
+            if (!((visit >> q) & 1u)) { w = shl_blk(w); continue; }
 #pragma unroll
             for (int j = 0; j < RL_BLK; ++j) {
                 cflt* mr = MD + 4 * (b0 + q * RL_BLK + j);

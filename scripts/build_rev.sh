@@ -11,7 +11,7 @@ mkdir -p "$out"
 cd "$tmp/practice_path_planning_for_formula_student_driverless_amd"
 flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I$tmp/include -Wno-unused-command-line-argument"
 for f in rl_kernels.hip rl_stream.hip rl_geom.hip rl_format.hip rl_abi.cpp; do
-  /opt/rocm/bin/hipcc $flags -c csrc/$f -o $tmp/$f.o &
+  /opt/rocm/bin/hipcc $flags -c csrc/$f -o $tmp/$f.o > /dev/null 2>&1 &
 done
 wait
 /opt/rocm/bin/hipcc $flags -shared $tmp/*.o -o "$out/librl_$name.so"
