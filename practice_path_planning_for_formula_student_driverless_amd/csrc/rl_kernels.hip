@@ -330,12 +330,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const bool tail_wave = wid_u >= ((Ta - 1) >> 6);
     // Open tracks without a partial chunk (OPEN_FAST): the boundary forms of DiffOpsOpen
     // (ref:560-579) touch samples 0, 1, N-2 and N-1 only, i.e. chunk positions k = 0, 1
-    // of lane 0 and K-2, K-1 of the last active lane.  Every lane evaluates the interior
-    // forms; a wave holding lane 0 or the last active lane (edge_wave, uniform) then
-    // re-evaluates those four positions with the general forms, which equal the interior
-    // ones on every other lane.
+    // of lane 0 (fl) and K-2, K-1 of the last active lane (ll).  Every lane evaluates the
+    // interior forms; in a wave holding one of those lanes (edge_wave, uniform) the four
+    // positions take their boundary coefficients and operands by lane-masked selects
+    // (eval_j / eval_grad below), so the boundary costs a few selects, not general forms
+    // with per-sample conditions (whose lane masks, held across the PGD loop, spilled).
     constexpr bool OPEN_FAST = !CLOSED && !RAGGED;
     const bool edge_wave = OPEN_FAST && (wid_u == 0 || wid_u == ((Ta - 1) >> 6));
+    const bool fl = tid == 0, ll = tid == Ta - 1;
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
@@ -838,7 +840,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             double am = (k > 0) ? a[k - 1] : lv;
             double ap = (k + 1 < K) ? a[k + 1] : rv;
             double x1, x2;
-            if (OPEN_FAST && !(edge_wave && (k == 0 || k == K - 1))) {   // interior forms (ref:563-575)
+            if (OPEN_FAST && edge_wave && (k == 0 || k == K - 1)) {
+                // D1 one-sided and D2 = 0 at sample 0 (fl, k = 0) and N-1 (ll, k = K-1)
+                // (ref:563-566, 573-575); the interior forms on every other lane
+                const bool e = (k == 0) ? fl : ll;
+                const double om = (k == 0 && fl) ? a[k] : am;
+                const double op = (k == K - 1 && ll) ? a[k] : ap;
+                x1 = (op - om) * (e ? invh : inv2h);
+                const double x2i = (sub2x(ap, a[k]) + am) * invh2;
+                x2 = e ? 0.0 : x2i;
+            } else if (OPEN_FAST) {             // interior forms (ref:563-575)
                 x1 = (ap - am) * inv2h;
                 x2 = (sub2x(ap, a[k]) + am) * invh2;
             } else {
@@ -895,10 +906,41 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             const double q1m = (k > 0) ? q1[k - 1] : l1, q1p = (k + 1 < K) ? q1[k + 1] : r1;
             const double q2m = (k > 0) ? q2[k - 1] : l2, q2p = (k + 1 < K) ? q2[k + 1] : r2;
             const double am = (k > 0) ? a1v[k - 1] : l3, ap = (k + 1 < K) ? a1v[k + 1] : r3;
-            if (OPEN_FAST && !(edge_wave && (k < 2 || k >= K - 2)))
+            if (OPEN_FAST && edge_wave && (k < 2 || k >= K - 2)) {
+                // the gathers of DiffOpsOpen at samples 0, 1 (fl) and N-2, N-1 (ll) in the
+                // interior shape (ref:567-578): a boundary form differs from it only in
+                // one term's coefficient and operand, and a term it lacks is added as c*0
+                // (the accumulator after 0.0 + x is never -0, so adding a zero leaves it)
+                const bool e = (k < 2) ? fl : ll;
+                double c1A = inv2h_x2, o1A = q1m, c1C = -inv2h_x2, o1C = q1p;
+                double o2A = q2m, o2B = q2[k], o2C = q2p;
+                double csA = inv2h, osA = am, csC = -inv2h, osC = ap;
+                if (k == 0) {                        // j = 0: -h^-1 v0, no D2T vm, v0 terms
+                    c1A = e ? -invh_x2 : c1A; o1A = e ? q1[k] : o1A;
+                    o2A = e ? 0.0 : o2A; o2B = e ? 0.0 : o2B;
+                    csA = e ? -invh : csA; osA = e ? a1v[k] : osA;
+                } else if (k == 1) {                 // j = 1: h^-1 vm, no D2T vm term
+                    c1A = e ? invh_x2 : c1A;
+                    o2A = e ? 0.0 : o2A;
+                    csA = e ? invh : csA;
+                } else if (k == K - 2) {             // j = N-2: -h^-1 vp, no D2T vp term
+                    c1C = e ? -invh_x2 : c1C;
+                    o2C = e ? 0.0 : o2C;
+                    csC = e ? -invh : csC;
+                } else {                             // j = N-1: +h^-1 v0, no D2T v0, vp terms
+                    c1C = e ? invh_x2 : c1C; o1C = e ? q1[k] : o1C;
+                    o2B = e ? 0.0 : o2B; o2C = e ? 0.0 : o2C;
+                    csC = e ? invh : csC; osC = e ? a1v[k] : osC;
+                }
+                const double g1 = (0.0 + c1A * o1A) + c1C * o1C;
+                const double g2 = ((0.0 + invh2_x2 * o2A) + m2invh2_x2 * o2B) + invh2_x2 * o2C;
+                const double gsm = (0.0 + csA * osA) + csC * osC;
+                g[k] = (g1 + g2) + lam2 * gsm;
+            } else if (OPEN_FAST) {
                 g[k] = grad_int(q1m, q1p, q2m, q2[k], q2p, am, ap);
-            else
+            } else {
                 g[k] = grad_at(k, q1m, q1[k], q1p, q2m, q2[k], q2p, am, a1v[k], ap);
+            }
         }
     };
 
@@ -1220,8 +1262,9 @@ static int cu_count() {
 
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
-#ifdef RL_ANALYZE_ONE   // static analysis builds (scripts/regs.sh -one): the C2/C3 shape only
-    return mintime ? launch_t<8, 256, true, true>(p, st) : launch_t<8, 256, true, false>(p, st);
+#ifdef RL_ANALYZE_ONE   // static analysis builds (scripts/regs_one.sh): the C2/C3 shape only (2: open)
+    constexpr bool CL = RL_ANALYZE_ONE != 2;
+    return mintime ? launch_t<8, 256, CL, true>(p, st) : launch_t<8, 256, CL, false>(p, st);
 #else
     if (p.N <= 4 * 64) return launch_kt<4, 64>(p, mintime, st);
     if (p.N <= 8 * 64) return launch_kt<8, 64>(p, mintime, st);      // one wave (single-wave paths)
