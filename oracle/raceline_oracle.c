@@ -264,7 +264,8 @@ typedef struct { double *a1, *a2, *r, *q1, *q2, *g1, *g2, *gsm, *D1a; } Work;
 /* eval_cost_grad_frozen ref:654-675 (gamma2==NULL) and
  * eval_cost_grad_timeweighted ref:866-895 (gamma2!=NULL) */
 static double cost_grad(const Ops* o, const double* A1, const double* A2, const double* N0, const double* W,
-                        const double* gamma2, double lambda, const double* alpha, double* grad, Work* w) {
+                        const double* gamma2, double lambda, const double* alpha, double* grad, Work* w,
+                        double* absJ) {
     int N = o->N;
     D1(o, alpha, w->a1);
     D2(o, alpha, w->a2);
@@ -274,6 +275,7 @@ static double cost_grad(const Ops* o, const double* A1, const double* A2, const 
     else { for (int i = 0; i < N; ++i) J += w->r[i] * w->r[i]; }
     double Jsm = 0;
     for (int i = 0; i < N; ++i) Jsm += w->a1[i] * w->a1[i];
+    *absJ = fabs(J) + fabs(lambda) * Jsm;   /* margin report: sum of |terms| (instrumentation) */
     J += lambda * Jsm;
     for (int i = 0; i < N; ++i) {
         double Wz = gamma2 ? W[i] * gamma2[i] * w->r[i] : W[i] * w->r[i];
@@ -385,6 +387,28 @@ static int state_alloc(State* s, int N) {
     return 0;
 }
 
+/* Decision-margin report (instrumentation, not in the reference).  The kernels compute J
+ * and the Armijo decrease from the same per-sample terms in another summation order (per
+ * lane, then a butterfly).  Two summations of the same n terms differ by at most
+ * 2*gamma(n+3)*sum|terms| (gamma(m) = m*u/(1-m*u), u = 2^-53; +3 covers the rounded
+ * products and the lambda*Jsm fold), and the comparison's own additions by a few u of
+ * their operands.  A decision whose margin exceeds that bound is taken the same way by any
+ * such summation: the report counts the decisions (Armijo tests ref:733 / 1009, stop tests
+ * ref:739 / 1022) and the smallest margin/bound ratio seen. */
+static double mg_min_ratio = INFINITY;
+static int64_t mg_n = 0, mg_below = 0;
+void oracle_margin_reset(void) { mg_min_ratio = INFINITY; mg_n = 0; mg_below = 0; }
+void oracle_margin_get(double* min_ratio, int64_t* n_decisions, int64_t* n_below) {
+    *min_ratio = mg_min_ratio; *n_decisions = mg_n; *n_below = mg_below;
+}
+static void mg_note(double margin, double bound) {
+    ++mg_n;
+    double r = (bound > 0) ? fabs(margin) / bound : (margin == 0 ? INFINITY : INFINITY);
+    if (r < mg_min_ratio) mg_min_ratio = r;
+    if (r <= 1.0) ++mg_below;
+}
+static double mg_gamma(int n) { const double u = 0x1p-53; return 2.0 * (n + 3) * u / (1.0 - (n + 3) * u); }
+
 /* compute_min_curvature_raceline ref:683-764 (mintime=0) and
  * compute_min_time_raceline ref:905-1052 (mintime=1), one instance. */
 static void run_instance(const rl_problem* pr, const rl_cfg* C, uint64_t seed, int mintime, State* s,
@@ -436,9 +460,12 @@ static void run_instance(const rl_problem* pr, const rl_cfg* C, uint64_t seed, i
             g2w = s->gamma2;
         }
         double step = C->step_init;                                                        /* ref:723 / 996 */
-        double J = cost_grad(&o, s->A1, s->A2, s->N0, s->W, g2w, C->lambda_smooth, s->alpha, s->grad, &s->w);
+        double absJ, absJn, absJprev;
+        double J = cost_grad(&o, s->A1, s->A2, s->N0, s->W, g2w, C->lambda_smooth, s->alpha, s->grad, &s->w, &absJ);
         int evals = 1, accepts = 0;
         double J_prev = J;
+        absJprev = absJ;
+        const double gam = mg_gamma(N), u = 0x1p-53;
         for (int it = 0; it < C->max_inner_iters; ++it) {                                  /* ref:727-742 */
             int accepted = 0, bt = 0;
             while (bt < 20) {
@@ -446,22 +473,31 @@ static void run_instance(const rl_problem* pr, const rl_cfg* C, uint64_t seed, i
                     double ai = s->alpha[i] - step * s->grad[i];
                     s->anew[i] = smin(s->hi[i], smax(s->lo[i], ai));
                 }
-                double Jn = cost_grad(&o, s->A1, s->A2, s->N0, s->W, g2w, C->lambda_smooth, s->anew, s->gnew, &s->w);
+                double Jn = cost_grad(&o, s->A1, s->A2, s->N0, s->W, g2w, C->lambda_smooth, s->anew, s->gnew, &s->w,
+                                      &absJn);
                 ++evals;
-                double dec = 0.0;
+                double dec = 0.0, absdec = 0.0;
                 for (int i = 0; i < N; ++i) dec += s->grad[i] * (s->anew[i] - s->alpha[i]);
+                for (int i = 0; i < N; ++i) absdec += fabs(s->grad[i] * (s->anew[i] - s->alpha[i]));
+                {
+                    const double cd = C->armijo_c * dec, rhs = J + cd;
+                    mg_note(rhs - Jn, gam * (absJn + absJ + fabs(C->armijo_c) * absdec) +
+                                          4.0 * u * (fabs(J) + fabs(cd) + fabs(Jn) + fabs(rhs)));
+                }
                 if (Jn <= J + C->armijo_c * dec) {
                     double* t = s->alpha; s->alpha = s->anew; s->anew = t;
                     t = s->grad; s->grad = s->gnew; s->gnew = t;
-                    J = Jn; accepted = 1; ++accepts;
+                    J = Jn; absJ = absJn; accepted = 1; ++accepts;
                     break;
                 }
                 step *= 0.5; bt++;
                 if (step < C->step_min) break;
             }
             if (!accepted) break;
+            mg_note(fabs(J_prev - J) - 1e-10, gam * (absJprev + absJ) + 4.0 * u * (fabs(J_prev) + fabs(J)));
             if (fabs(J_prev - J) < 1e-10) break;
             J_prev = J;
+            absJprev = absJ;
         }
         if (out->evals) out->evals[(size_t)b * MO + outer] = evals;
         if (out->accepts) out->accepts[(size_t)b * MO + outer] = accepts;

@@ -43,6 +43,10 @@ def oracle() -> C.CDLL:
         lib.oracle_vpass.argtypes = [C.POINTER(abi.RlCfg), C.POINTER(C.c_double), C.c_int, C.c_double, C.c_int,
                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32)]
         lib.oracle_vpass.restype = C.c_double
+        lib.oracle_margin_reset.argtypes = []
+        lib.oracle_margin_reset.restype = None
+        lib.oracle_margin_get.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        lib.oracle_margin_get.restype = None
         lib.oracle_ring_segments.argtypes = [C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_double)]
         lib.oracle_ring_segments.restype = C.c_int
         lib.oracle_geom.argtypes = [C.POINTER(abi.RlGeomProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double)]
