@@ -61,6 +61,9 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 // inner iteration is rejected (both optimisers)
 // corridor samples per lane in the streaming kernel (C5 A/B: 1 -> 36.0 ms, 2 -> 32.4 ms,
 // 4 -> 41.6 ms; scripts/ab_c5.py)
+#ifndef RL_SFUSE
+#define RL_SFUSE 1       // lin-geom (and min-time curvature) in the normals pass (A/B knob)
+#endif
 #ifndef RL_SCK
 #define RL_SCK 2
 #endif
@@ -206,6 +209,20 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         if (!(n < 1e-15)) { ox = vx / n; oy = vy / n; }
         NX[i] = ox;
         NY[i] = oy;
+#if RL_SFUSE
+        // precompute_lin_geom_generic (ref:622-651) at i in the same pass over P: it needs
+        // only this sample's normal, so the later lin-geom pass (and, for min-time, the
+        // curvature pass, ref:595-620) need not read P and n again
+        double xp, yp, xpp, ypp;
+        deriv(i, xp, yp, xpp, ypp);
+        CA1[i] = ox * ypp - oy * xpp;
+        CA2[i] = xp * oy - yp * ox;
+        const double n0 = xp * ypp - yp * xpp;
+        CN0[i] = n0;
+        const double d = pow15(smax(1e-12, xp * xp + yp * yp));
+        CW[i] = 1.0 / d;
+        if (MT) KA[i] = n0 / d;
+#endif
     };
     // corridor (ref:694-711 / 749-756) at sample i via the per-lane candidate scan
     auto corridor_at = [&](int i, double guard) {
@@ -422,7 +439,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         __syncthreads();
 #endif
         RL_SSTAMP(1);
-        if (MT || outer == MO) {
+        if ((MT && !RL_SFUSE) || outer == MO) {
             for (int i = tid; i < N; i += TS) {                    // ref:595-620
                 double xp, yp, xpp, ypp;
                 deriv(i, xp, yp, xpp, ypp);
@@ -475,14 +492,16 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         RL_SSTAMP(2);
         if (outer == MO) break;
 
-        for (int i = tid; i < N; i += TS) {                        // ref:622-651
-            double xp, yp, xpp, ypp;
-            deriv(i, xp, yp, xpp, ypp);
-            const double nx = NX[i], ny = NY[i];
-            CA1[i] = nx * ypp - ny * xpp;
-            CA2[i] = xp * ny - yp * nx;
-            CN0[i] = xp * ypp - yp * xpp;
-            CW[i] = 1.0 / pow15(smax(1e-12, xp * xp + yp * yp));
+        if (!RL_SFUSE) {
+            for (int i = tid; i < N; i += TS) {                    // ref:622-651
+                double xp, yp, xpp, ypp;
+                deriv(i, xp, yp, xpp, ypp);
+                const double nx = NX[i], ny = NY[i];
+                CA1[i] = nx * ypp - ny * xpp;
+                CA2[i] = xp * ny - yp * nx;
+                CN0[i] = xp * ypp - yp * xpp;
+                CW[i] = 1.0 / pow15(smax(1e-12, xp * xp + yp * yp));
+            }
         }
         __syncthreads();
         RL_SSTAMP(3);

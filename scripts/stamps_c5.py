@@ -11,16 +11,17 @@ names = ["setup", "corridor tail (write, seed)", "mt:κ/vpass/γ", "lin-geom", "
          "corridor loads", "corridor: inner-ring rays", "corridor: outer-ring rays", "corridor: fallback search",
          "-", "-", "-", "-", "-"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+MODE = int(sys.argv[2]) if len(sys.argv) > 2 else 1      # 1 min-curv, 2 min-time
 case = O.load_case("oval_n10000"); prob = O.case_problem(case); cfg = O.case_cfg(case)
 h = C.c_void_p(); p = prob.as_c(); arr, n = abi.cfg_array(cfg)
 seeds = np.arange(B, dtype=np.uint64)
-assert lib.rl_plan_create(C.byref(h), 0, C.byref(p), arr, n, abi.u64ptr(seeds), B, 1) == 0
+assert lib.rl_plan_create(C.byref(h), 0, C.byref(p), arr, n, abi.u64ptr(seeds), B, MODE) == 0
 assert lib.rl_plan_run(h, None) == 0
-ms = C.c_float(); lib.rl_plan_kernel_ms(h, 1, C.byref(ms))
+ms = C.c_float(); lib.rl_plan_kernel_ms(h, MODE, C.byref(ms))
 st = np.zeros((B, 16), dtype=np.uint64)
 assert lib.rl_debug_stamps_stream(st.ctypes.data_as(C.c_void_p), B) == 0
 tot = st.sum(0).astype(float)
-print(f"C5 B={B} kernel {ms.value:.2f} ms; per-block cycles {tot.sum()/B:.3e}")
+print(f"C5 mode={MODE} B={B} kernel {ms.value:.2f} ms; per-block cycles {tot.sum()/B:.3e}")
 for i, nm in enumerate(names):
     if tot[i] > 0: print(f"   {nm:30s} {100*tot[i]/tot.sum():5.1f}%  {tot[i]/B:.3e} cyc/block")
 lib.rl_plan_destroy(h)
