@@ -19,6 +19,7 @@
 //     then the 16 wave partials in order.
 // This is the HBM-bound configuration; its roofline is HBM bytes.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "rl_abi.h"
@@ -63,6 +64,15 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 // 4 -> 41.6 ms; scripts/ab_c5.py)
 #ifndef RL_SFUSE
 #define RL_SFUSE 1       // lin-geom (and min-time curvature) in the normals pass (A/B knob)
+#endif
+#ifndef RL_SVP_REG
+#define RL_SVP_REG 1     // register-resident v-pass for RL_SVP_MIN <= ceil(N/1024) <= RL_SVP_MAX (A/B knob)
+#endif
+#ifndef RL_SVP_MIN
+#define RL_SVP_MIN 5
+#endif
+#ifndef RL_SVP_MAX
+#define RL_SVP_MAX 12
 #endif
 #ifndef RL_SCK
 #define RL_SCK 2
@@ -358,6 +368,144 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         return sweeps;
     };
 
+    // Register-resident v-pass for Cr = CR samples per thread (RL_SVP_MIN <= Cr <= RL_SVP_MAX,
+    // e.g. C5's N = 10000: Cr = 10).  The chunk's κ, its values and the pass-start values stay
+    // in registers for the whole v pass (the memory path above reloads them from HBM in every
+    // relaxation round), and a re-evaluated chunk stops at the first value that repeats bit for
+    // bit (each step depends only on the previous value: the rest would repeat, its outgoing
+    // value included).  Rounds end when no published value changes.  Padding slots of the
+    // partial last chunk hold ka = 0, v = +inf and never bind.  Same fixed point, bit for bit.
+    auto same_bits = [](double a, double b) -> bool { return __double_as_longlong(a) == __double_as_longlong(b); };
+    auto vpass_reg = [&](auto crc) -> int {
+        constexpr int CR = decltype(crc)::value;
+        const VConst vc = sm.vc;
+        const int cnt = r1 - r0;                  // CR, except the last active thread; 0 beyond N
+        double ka[CR], v[CR];
+#pragma unroll
+        for (int k = 0; k < CR; ++k) {
+            ka[k] = 0.0;
+            if (k < cnt) ka[k] = KA[r0 + k];
+            const double kk = fabs(ka[k]);
+            const double vk = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
+            v[k] = (k < cnt) ? vk : INFINITY;
+        }
+        int sweeps = 0;
+        for (int s = 0; s < C.max_vpass_iters; ++s) {
+            ++sweeps;
+            bool any = false;
+            {   // forward (ref:829-833)
+                double vst[CR];
+#pragma unroll
+                for (int k = 0; k < CR; ++k) vst[k] = v[k];
+                double in_prev = -1.0, out = INFINITY;
+                for (int it = 0;; ++it) {
+                    double in = INFINITY;
+                    if (it > 0 && has_left) in = sm.vin[(it - 1) & 1][tid - 1];
+                    bool ch = false;
+                    if (ract && in != in_prev) {
+                        in_prev = in;
+                        const double cur = has_left ? smin(vst[0], in) : vst[0];
+                        bool go = it == 0 || !same_bits(cur, v[0]);
+                        v[0] = cur;
+#pragma unroll
+                        for (int k = 0; k + 1 < CR; ++k) {
+                            if (!__any(go)) break;
+                            if (go) {
+                                const double vf = vstep_fwd(vc, v[k], ka[k]);
+                                const double nv = (k + 1 < cnt) ? smin(vst[k + 1], vf) : INFINITY;
+                                go = it == 0 || !same_bits(nv, v[k + 1]);
+                                v[k + 1] = nv;
+                            }
+                        }
+                        if (has_right && go) {             // has_right => full chunk
+                            const double o = vstep_fwd(vc, v[CR - 1], ka[CR - 1]);
+                            ch = o != out;
+                            out = o;
+                        }
+                    }
+                    if (has_right) sm.vin[it & 1][tid] = out;
+                    if (!__syncthreads_or(ch) && it > 0) break;
+                }
+                if (CLOSED) {                                  // ref:834-839
+                    if (ract && r1 == N) {
+                        double vl = v[0], kl = ka[0];
+#pragma unroll
+                        for (int k = 1; k < CR; ++k)
+                            if (k == cnt - 1) { vl = v[k]; kl = ka[k]; }
+                        sm.bc[0] = vstep_fwd(vc, vl, kl);
+                    }
+                    __syncthreads();
+                    if (tid == 0) v[0] = smin(v[0], sm.bc[0]);
+                }
+#pragma unroll
+                for (int k = 0; k < CR; ++k) any |= (k < cnt) && (v[k] != vst[k]);
+            }
+            {   // backward (ref:841-845)
+                double vpre[CR];
+#pragma unroll
+                for (int k = 0; k < CR; ++k) vpre[k] = v[k];
+                __syncthreads();                               // vin reuse: the forward reads are done
+                double in_prev = -1.0, out = INFINITY;
+                for (int it = 0;; ++it) {
+                    double in = INFINITY;
+                    if (it > 0 && has_right) in = sm.vin[(it - 1) & 1][tid + 1];
+                    bool ch = false;
+                    if (ract && in != in_prev) {
+                        in_prev = in;
+                        const double cur = has_right ? smin(vpre[CR - 1], in) : vpre[CR - 1];
+                        bool go = it == 0 || !same_bits(cur, v[CR - 1]);
+                        v[CR - 1] = cur;
+#pragma unroll
+                        for (int k = CR - 2; k >= 0; --k) {
+                            if (!__any(go)) break;
+                            if (go) {
+                                const double vb = vstep_bwd(vc, v[k + 1], ka[k + 1]);
+                                const double nv = (k < cnt) ? smin(vpre[k], vb) : INFINITY;
+                                go = it == 0 || !same_bits(nv, v[k]);
+                                v[k] = nv;
+                            }
+                        }
+                        if (has_left && go) {
+                            const double o = vstep_bwd(vc, v[0], ka[0]);
+                            ch = o != out;
+                            out = o;
+                        }
+                    }
+                    if (has_left) sm.vin[it & 1][tid] = out;
+                    if (!__syncthreads_or(ch) && it > 0) break;
+                }
+                if (CLOSED) {                                  // ref:846-850
+                    if (tid == 0) sm.bc[1] = vstep_bwd(vc, v[0], ka[0]);
+                    __syncthreads();
+                    if (ract && r1 == N) {
+#pragma unroll
+                        for (int k = 0; k < CR; ++k)
+                            if (k == cnt - 1) v[k] = smin(v[k], sm.bc[1]);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < CR; ++k) any |= (k < cnt) && (v[k] != vpre[k]);
+            }
+            if (!__syncthreads_or(any)) break;                 // later sweeps are exact repeats
+        }
+#pragma unroll
+        for (int k = 0; k < CR; ++k)
+            if (k < cnt) V[r0 + k] = v[k];
+        return sweeps;
+    };
+    auto vpass_any = [&]() -> int {
+        if (RL_SVP_REG) {
+            switch (Cr) {
+#define RL_SVP_CASE(n) case n: if (n >= RL_SVP_MIN && n <= RL_SVP_MAX) return vpass_reg(std::integral_constant<int, n>()); break;
+                RL_SVP_CASE(5) RL_SVP_CASE(6) RL_SVP_CASE(7) RL_SVP_CASE(8)
+                RL_SVP_CASE(9) RL_SVP_CASE(10) RL_SVP_CASE(11) RL_SVP_CASE(12)
+#undef RL_SVP_CASE
+                default: break;
+            }
+        }
+        return vpass();
+    };
+
     // ---- init ---------------------------------------------------------------
     for (int i = tid; i < N; i += TS) {
         X[i] = CEN[2 * i];
@@ -449,7 +597,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             __syncthreads();
         }
         if (MT) {
-            const int sw = vpass();                                // ref:947 / 1047
+            const int sw = vpass_any();                            // ref:947 / 1047
             if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
             __syncthreads();
             if (outer == MO) {

@@ -33,6 +33,7 @@ VARIANTS = {
     "blk8": {"RL_BLKSZ": 8},
     "blk32": {"RL_BLKSZ": 32},
     "nofuse": {"RL_SFUSE": 0},
+    "svp0": {"RL_SVP_REG": 0},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }

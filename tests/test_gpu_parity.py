@@ -316,7 +316,7 @@ def test_reference_shaped_calls():
 
 
 @pytest.mark.parametrize("closed", [True, False])
-@pytest.mark.parametrize("N", [1, 2, 3, 5, 64, 1000, 1025, 2047, 4097])
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 64, 1000, 1025, 2047, 4097, 6143, 12288])
 def test_streaming_kernel_vs_oracle(N, closed, monkeypatch):
     """The large-N streaming kernel (forced for small N too) against the oracle."""
     _lib_or_skip()
