@@ -510,8 +510,8 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     for (int i = tid; i < N; i += TS) {
         X[i] = CEN[2 * i];
         Y[i] = CEN[2 * i + 1];
-        ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0; GR[i] = 0.0;
-    }
+        ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0;   // (the gradient needs no zeroing: each outer
+    }                                                     // iteration's first evaluation writes it first)
     const int MO = C.max_outer_iters;
     double* al_p = AL;
     double* an_p = AN;
@@ -526,7 +526,6 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 Y[i] += NY[i] * a;
                 ATOT[i] += a;
                 al_p[i] = 0.0;                                     // ref:757
-                GR[i] = 0.0;
             }
             __syncthreads();
         }
