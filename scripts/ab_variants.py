@@ -37,8 +37,14 @@ CASES = [("C2", "cmap1_n2000", 1024, 1, 1, False), ("C3mt", "cmap1_n2000_vp20", 
          ("C3big", "cmap1_n2000_vp20", 4096, 2, 2, True), ("C5", "oval_n10000", 1024, 1, 1, False),
          ("C5mt", "oval_n10000", 1024, 2, 2, True), ("C4t3", "track_competition_map_testday3", 512, 3, 0, True)]
 sel = os.environ.get("AB_CASES")
-CASES += [("O2", "open:cmap1_n2000", 1024, 1, 1, False), ("O2mt", "open:cmap1_n2000", 1024, 2, 2, True)]
+CASES += [("O2", "open:cmap1_n2000", 1024, 1, 1, False), ("O2mt", "open:cmap1_n2000", 1024, 2, 2, True),
+          # the streaming kernel forced on C2's problem: the accepting regime (E_k 135, 120 accepts)
+          ("S2", "cmap1_n2000", 1024, 1, 1, False), ("S2mt", "cmap1_n2000", 1024, 2, 2, True)]
 for cname, cfgname, B, modes, idx, mt in [c for c in CASES if not sel or c[0] in sel.split(",")]:
+    if cname.startswith("S"):
+        os.environ["RL_FORCE_STREAM"] = "1"
+    else:
+        os.environ.pop("RL_FORCE_STREAM", None)
     if cfgname.startswith("open:"):      # C2's track as an open path (bench.py open_problem)
         import bench
         prob, cfg = bench.open_problem()
