@@ -165,6 +165,23 @@ def test_n2000_mintime_throughput_shape(closed):
     np.testing.assert_allclose(mt.lap[pick], smt.lap, rtol=1e-13, atol=0)
 
 
+def test_open_track_n2000_throughput_shapes():
+    """C2's track as an open path (the bench's open-mode line) at B=512: min-curv and min-time
+    both run the (8, 256) shape without a partial chunk, whose DiffOpsOpen boundary stencils
+    (ref:560-579) are lane-masked selects in edge waves 0 and 3 (the last active lane is
+    lane 57 of wave 3).  Three seeds against the oracle, counters exact."""
+    _lib_or_skip()
+    import bench
+    prob, cfg = bench.open_problem()
+    B = 512
+    seeds = np.arange(B, dtype=np.uint64)
+    mc, mt = raceline.optimize_batch(prob, cfg, seeds, B)
+    pick = np.array([0, 11, 300])
+    omc, omt = O.run_oracle(prob, cfg, seeds=seeds[pick], B=len(pick))
+    compare_outputs(_pick_rows(mc, pick, False), omc, False, "open n2000.mc")
+    compare_outputs(_pick_rows(mt, pick, True), omt, True, "open n2000.mt")
+
+
 def _synthetic(N, closed, rng):
     t = np.linspace(0, 2 * np.pi, N, endpoint=False)
     r = 20 + rng.uniform(-0.05, 0.05, N)
