@@ -403,7 +403,8 @@ void oracle_margin_get(double* min_ratio, int64_t* n_decisions, int64_t* n_below
 }
 static void mg_note(double margin, double bound) {
     ++mg_n;
-    double r = (bound > 0) ? fabs(margin) / bound : (margin == 0 ? INFINITY : INFINITY);
+    /* bound 0: every term is an exact zero, so any summation gives the same zero sums */
+    double r = (bound > 0) ? fabs(margin) / bound : INFINITY;
     if (r < mg_min_ratio) mg_min_ratio = r;
     if (r <= 1.0) ++mg_below;
 }
