@@ -197,12 +197,14 @@ def _synthetic(N, closed, rng):
 
 
 @pytest.mark.parametrize("closed", [True, False])
-@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 1000, 1023, 1025, 1536, 2047, 2048, 2049,
-                               3072, 4096])
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 8, 63, 64, 65, 255, 256, 257, 392, 512, 1000, 1023, 1025, 1536, 2047,
+                               2048, 2049, 3072, 4096])
 def test_ragged_sizes_vs_oracle(N, closed):
-    """Every kernel variant (K,T) and every partial-chunk shape, closed and open.  The
-    multiples of K with three or more waves per instance (1536, 2048, 3072, 4096) run the
-    open interior-stencil path in waves that hold no boundary sample."""
+    """Every kernel variant (K,T) and every partial-chunk shape, closed and open.  Open
+    multiples of K take the interior stencils with the boundary selects (rl_kernels.hip
+    OPEN_FAST): one lane holding both ends (4, 8), a single wave with its last active lane
+    inside (392) or at lane 63 (512), and three or more waves per instance (1536, 2048,
+    3072, 4096), whose middle waves hold no boundary sample."""
     _lib_or_skip()
     rng = np.random.default_rng(N)
     prob = _synthetic(N, closed, rng)
