@@ -32,11 +32,11 @@ import time
 
 import numpy as np
 
-# HIP hardware queues for this process (HIP's default is 4): the C4 line runs 7 plans with
-# both modes concurrently (14 streams); with 4 queues the streams share queues and serialise
-# (C4 23.3 ms), with 16 they run side by side (18.4 ms; scripts/c4_sched.py).  Read by the
-# HIP runtime at initialisation, so it is set before anything touches HIP.
-os.environ["GPU_MAX_HW_QUEUES"] = "16"     # the box exports 4 (HIP's default); <= 32 is allowed
+# HIP hardware queues of this process: the operator's setting is kept (the GPU box exports
+# HIP's default, 4); only when nothing is set does the bench ask for 16.  The value is
+# recorded in the JSON line (`hip_hw_queues`): the C4 line's concurrent plans are scheduled
+# onto that many streams (run_c4).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -116,50 +116,12 @@ def _cpu_info() -> dict:
     return {"model": model, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
 
-class _RefHarness:
-    """oracle/_ref/libref_harness.so: the reference's own main.cpp compiled from its
-    sources (oracle/Makefile `ref`, built in the build container; absent -> None)."""
-
-    def __init__(self):
-        import ctypes as C
-
-        import oracle_lib as O
-
-        self.C = C
-        self.lib = C.CDLL(O.REF_SO)
-        d = C.POINTER(C.c_double)
-        common = [d, C.c_int, C.c_double, C.c_int, d, C.c_int, d, C.c_int, C.c_double] + [d] * 6
-        self.lib.ref_min_curv.argtypes = common
-        self.lib.ref_min_time.argtypes = common + [d, d, d]
-        self.lib.ref_cfg_apply.argtypes = [C.POINTER(abi.RlCfg)]
-        self.lib.ref_cfg_reset()
-
-    def run(self, prob, cfg, mintime: bool) -> float:
-        """One compute_min_curvature_raceline / compute_min_time_raceline call (ref:683 /
-        905) on the problem; returns the lap (min-time) or 0."""
-        C = self.C
-        self.lib.ref_cfg_reset()
-        self.lib.ref_cfg_apply(C.byref(cfg))
-        N = prob.N
-        outs = [np.zeros(max(N, 1)) for _ in range(8)]
-        lap = np.zeros(1)
-        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))   # noqa: E731
-        args = [dp(np.ascontiguousarray(prob.center)), N, prob.L, 1 if prob.closed else 0,
-                dp(np.ascontiguousarray(prob.inner_seg)), prob.inner_seg.shape[0],
-                dp(np.ascontiguousarray(prob.outer_seg)), prob.outer_seg.shape[0], prob.veh_width]
-        if mintime:
-            rc = self.lib.ref_min_time(*args, *[dp(o) for o in outs], dp(lap))
-        else:
-            rc = self.lib.ref_min_curv(*args, *[dp(o) for o in outs[:6]])
-        if rc != 0:
-            raise RuntimeError("reference harness failed")
-        return float(lap[0])
-
-
-def _ref_harness():
+def _ref_bench_available() -> bool:
+    """oracle/_ref/ref_bench_o3: the reference's own main.cpp built from its sources with
+    its README's flags (oracle/Makefile `ref`, built in the build container)."""
     import oracle_lib as O
 
-    return _RefHarness() if os.path.exists(O.REF_SO) else None
+    return os.path.exists(O.REF_BENCH)
 
 
 def _lap_worker(job):
@@ -185,25 +147,37 @@ def cpu_leg(budget_s: float) -> dict:
 
     import oracle_lib as O
 
+    import tempfile
+
     cores = sorted(os.sched_getaffinity(0))
     os.sched_setaffinity(0, {cores[0]})
     info = _cpu_info()
     res = {"cpu": info}
     case, prob, cfg = load_problem("cmap1_n2000")
     MO = int(cfg.max_outer_iters)
-    ref = _ref_harness()
-    # ---- baseline: C2 min-curvature at N=2000 on one core
-    if ref is not None:
-        n, t0 = 0, time.perf_counter()
-        while n == 0 or time.perf_counter() - t0 < budget_s:
-            ref.run(prob, cfg, False)
-            n += 1
-        dt = time.perf_counter() - t0
+    have_ref = _ref_bench_available()
+    work = tempfile.mkdtemp(prefix="rl_cpu_leg_")
+    # ---- baseline: C2 min-curvature at N=2000 on one core, the reference as its README builds it
+    if have_ref:
+        r = O.run_ref_bench(prob, cfg, False, budget_s, 3, work)
+        n, dt = int(r["calls"]), float(r["seconds"])
+        c3case, p3, cfg3 = load_problem("cmap1_n2000_vp20")
+        rt = O.run_ref_bench(p3, cfg3, True, budget_s / 3, 2, work)
         res["reference"] = {"value": n * MO / dt, "unit": "PGD outer-iters/s", "cores": 1, "kind": "reference",
-                            "sample": f"{n} calls of the reference's compute_min_curvature_raceline (main.cpp:683-764, "
-                                      f"oracle/_ref built from /root/reference/src/main.cpp) on C2's problem "
-                                      f"(competition_map1, N={prob.N}, alpha=0 start), {MO} outer each, {dt:.1f} s, "
-                                      f"one thread pinned to core {cores[0]}"}
+                            "build": O.ref_bench_build(),
+                            "sample": f"{n} calls of the reference's compute_min_curvature_raceline (main.cpp:683-764; "
+                                      f"oracle/_ref/ref_bench_o3 = /root/reference/src/main.cpp built with its README's "
+                                      f"g++ -std=c++17 -O3) on C2's problem (competition_map1, N={prob.N}, alpha=0 "
+                                      f"start), {MO} outer each, {dt:.1f} s, one thread pinned to core {cores[0]}",
+                            "ms_per_call_median": float(np.median(r["ms"])),
+                            "x0_equals_reference_fixture": r["x0"] == float(case["mc_x"][0]),
+                            "mintime_c3_problem": {
+                                "value": int(rt["calls"]) * int(cfg3.max_outer_iters) / float(rt["seconds"]),
+                                "unit": "PGD outer-iters/s", "calls": int(rt["calls"]),
+                                "ms_per_call_median": float(np.median(rt["ms"])),
+                                "lap_equals_reference_fixture": rt["lap"] == float(c3case["mt_lap"]),
+                                "sample": "compute_min_time_raceline (main.cpp:905-1052) on C3's problem "
+                                          "(competition_map1, N=2000, max_vpass_iters=20), same build and core"}}
     n, t0 = 0, time.perf_counter()
     seeds = np.arange(256, dtype=np.uint64)
     while n < len(seeds) and (n == 0 or time.perf_counter() - t0 < budget_s / 2):
@@ -214,15 +188,12 @@ def cpu_leg(budget_s: float) -> dict:
                    "sample": f"{n} C2 instances (seeds 0..{n - 1}) through the C restatement of main.cpp:683-1052 "
                              f"(oracle/raceline_oracle.c), {dt:.1f} s, one thread pinned to core {cores[0]}"}
     # ---- the drop-in use (one instance per call, ref:1347 / 1397): the reference per track
-    if ref is not None:
+    # (median of 3 calls, same build and core)
+    if have_ref:
         per = {}
         for name in DROPIN_CASES:
             _, p, c = load_problem(name)
-            ts = []
-            for mintime in (False, True):
-                t0 = time.perf_counter()
-                ref.run(p, c, mintime)
-                ts.append(1e3 * (time.perf_counter() - t0))
+            ts = [float(np.median(O.run_ref_bench(p, c, mt, 0.0, 3, work)["ms"])) for mt in (False, True)]
             per[name] = {"N": p.N, "mincurv_ms": round(ts[0], 2), "mintime_ms": round(ts[1], 2)}
         res["reference_per_track"] = per
     # ---- oracle laps for the lap-Δ statistics (C3 sample, the whole C4 grid)
@@ -249,6 +220,9 @@ def cpu_leg(budget_s: float) -> dict:
     omc, omt = O.run_oracle(oprob, ocfg, seeds=list(range(OPEN_CHECK)), B=OPEN_CHECK)
     res["open_oracle"] = {"x": omc.x.tolist(), "evals": omc.evals.tolist(), "lap": omt.lap.tolist(),
                           "mt_evals": omt.evals.tolist()}
+    import shutil
+
+    shutil.rmtree(work, ignore_errors=True)
     return res
 
 
@@ -346,18 +320,23 @@ def run_c3(rank, local, stream, reps: int = 3):
 
 def run_c4(world, rank, local, dev, dist):
     """C4: 7 bundled tracks x 512 (mu, P_max_W, lambda_smooth) points, min-curv + min-time.
-    Items are sharded track-major over ranks; one plan per track, all plans on
-    concurrent HIP streams; laps gathered to rank 0 in item order."""
+    Items are sharded track-major over ranks; one plan per (track, mode), every plan on its
+    own HIP stream, all enqueued before any wait; laps gathered to rank 0 in item order.
+    (scripts/c4_sched2.py at the box's 4 hardware queues: one plan per track with both modes
+    on 7 streams 23.1 ms, these 14 single-mode plans 18.3 ms -- as fast as 16 queues.)"""
     import torch
 
     groups = D.c4_shard(world, rank)
     base = load_problem("track_training_map")[2]
     cfgs = D.c4_cfgs(base)
-    plans, meta = [], []
+    plans, mt_plans, meta = [], [], []
     for t, ks in groups.items():
         case, prob, _ = load_problem("track_" + D.C4_TRACKS[t])
-        plans.append(raceline.Plan(prob, [cfgs[k] for k in ks], B=len(ks),
-                                   modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, device=local))
+        for mode in (abi.RL_MODE_MINCURV, abi.RL_MODE_MINTIME):
+            pl = raceline.Plan(prob, [cfgs[k] for k in ks], B=len(ks), modes=mode, device=local)
+            plans.append(pl)
+            if mode == abi.RL_MODE_MINTIME:
+                mt_plans.append(pl)
         meta.append((t, ks, prob))
     streams = [torch.cuda.Stream(device=dev) for _ in plans]
 
@@ -376,7 +355,7 @@ def run_c4(world, rank, local, dev, dist):
         launch()
     dt = (time.perf_counter() - t0) / reps
     n_inst = sum(len(ks) for _, ks, _ in meta)
-    laps = np.concatenate([pl.fetch()[1].lap for pl in plans])
+    laps = np.concatenate([pl.fetch()[1].lap for pl in mt_plans])
     for pl in plans:
         pl.close()
     if dist is not None:
@@ -479,17 +458,20 @@ def run_dropin(local):
                 t0 = time.perf_counter()
                 raceline.optimize_batch(prob, cfg, None, 1, mincurv=mode == "mincurv", mintime=mode == "mintime")
                 t[mode].append(1e3 * (time.perf_counter() - t0))
-                km, cm = C.c_float(), C.c_float()
-                lib.rl_last_call_ms(C.byref(km), C.byref(cm))
-                k[mode].append((km.value, cm.value))
+                run, kmc, kmt, cm = C.c_float(), C.c_float(), C.c_float(), C.c_float()
+                lib.rl_last_call_times(C.byref(run), C.byref(kmc), C.byref(kmt), C.byref(cm))
+                k[mode].append((run.value, kmc.value if mode == "mincurv" else kmt.value, cm.value))
         med = lambda v: round(float(np.median(v)), 3)   # noqa: E731
-        out[name] = {"N": prob.N, "mincurv_ms": med(t["mincurv"]), "mintime_ms": med(t["mintime"])}
+        out[name] = {"N": prob.N, "mincurv_ms": med(t["mincurv"]), "mintime_ms": med(t["mintime"]),
+                     "shape_KxT": {m: "x".join(map(str, abi.kernel_shape(prob.N, 1, mode)))
+                                   for m, mode in (("mincurv", abi.RL_MODE_MINCURV), ("mintime", abi.RL_MODE_MINTIME))}}
         for mode in ("mincurv", "mintime"):
-            out[name][mode + "_kernel_ms"] = med([a for a, _ in k[mode]])
-            # inside the C call, outside the kernels: uploads, launch, downloads, host copies
-            out[name][mode + "_abi_overhead_ms"] = med([c - a for a, c in k[mode]])
+            # the optimiser kernel alone (its own start/end events)
+            out[name][mode + "_kernel_ms"] = med([m for _, m, _ in k[mode]])
+            # inside the C call, outside the run bracket: uploads, launch, downloads, host copies
+            out[name][mode + "_abi_overhead_ms"] = med([c - r for r, _, c in k[mode]])
             # the Python wrapper's own share (numpy output allocation, ctypes marshalling)
-            out[name][mode + "_python_ms"] = med([w - c for w, (_, c) in zip(t[mode], k[mode])])
+            out[name][mode + "_python_ms"] = med([w - c for w, (_, _, c) in zip(t[mode], k[mode])])
     return out
 
 
@@ -514,15 +496,16 @@ def run_c2_pcie(prob, cfg, B, MO, rank):
             out = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
             ts.append(time.perf_counter() - t0)
             del out                  # the caller keeps its results: freeing them is not part of the call
-            km, cm = C.c_float(), C.c_float()
-            lib.rl_last_call_ms(C.byref(km), C.byref(cm))
-            ks.append((km.value, cm.value))
+            run, kmc, cm = C.c_float(), C.c_float(), C.c_float()
+            lib.rl_last_call_times(C.byref(run), C.byref(kmc), None, C.byref(cm))
+            ks.append((run.value, kmc.value, cm.value))
     finally:
         os.sched_setaffinity(0, prev)
     t = float(np.median(ts))
     return {"call_ms_median": round(t * 1e3, 2), "outer_iters_per_s": round(B * MO / t, 1),
-            "kernel_ms_median": round(float(np.median([k for k, _ in ks])), 3),
-            "abi_call_ms_median": round(float(np.median([c for _, c in ks])), 3),
+            "run_bracket_ms_median": round(float(np.median([r for r, _, _ in ks])), 3),
+            "kernel_ms_median": round(float(np.median([k for _, k, _ in ks])), 3),
+            "abi_call_ms_median": round(float(np.median([c for _, _, c in ks])), 3),
             "host_cores": len(spare) + len(prev),
             "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8)}
 
@@ -620,9 +603,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # the CPU leg (rank 0 at N=1 only) starts before this process touches the GPU
+    # the CPU leg (rank 0, any world size) starts before this process touches the GPU; the
+    # other ranks keep off its pinned core
     HOST_CORES.update(os.sched_getaffinity(0))
-    cpu_proc = start_cpu_leg(args.cpu_budget) if (world == 1 and not args.no_cpu and not args.no_extras) else None
+    cpu_proc = start_cpu_leg(args.cpu_budget) if (rank == 0 and not args.no_cpu and not args.no_extras) else None
+    if rank != 0 and len(HOST_CORES) > 2:
+        os.sched_setaffinity(0, set(HOST_CORES) - {min(HOST_CORES)})
     # rehearsal on a one-GPU box only: every rank on cuda:0, gloo instead of RCCL
     if os.environ.get("RL_BENCH_SAME_DEVICE") == "1":
         local = 0
@@ -824,6 +810,7 @@ def main():
                    "global_batch": world * B, "parallelism": f"dp{world}: instances sharded over {world} GPU(s); per-step RCCL gather of "
                                   f"per-instance summaries to rank 0"},
         "tracks_per_s": round(tracks_per_s, 2),
+        "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity if summary_check is None else {**parity, "gather": summary_check},

@@ -165,8 +165,18 @@ int rl_optimize(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
  * time from the first to the last kernel of the call, *call_ms = wall time of the whole
  * call (uploads, kernels, downloads into the caller's buffers).  Either may be NULL.    */
 int rl_last_call_ms(float* kernel_ms, float* call_ms);
+/* The same call's times split: *run_ms = the run bracket (as rl_last_call_ms' kernel_ms:
+ * first kernel start to last kernel end), *mincurv_ms / *mintime_ms = each optimiser kernel
+ * alone from its own start and end events (-1 when that mode did not run), *call_ms = wall
+ * time of the whole call.  Any pointer may be NULL. */
+int rl_last_call_times(float* run_ms, float* mincurv_ms, float* mintime_ms, float* call_ms);
 /* Free the idle plans and pinned buffers of the cache (device memory returns to HIP). */
 int rl_release_plan_cache(void);
+/* Idle plans in the cache and the device / pinned host bytes they hold.  The cache keeps
+ * at most 8 idle plans and RL_PLAN_CACHE_MB (environment, default 2048) MiB of device plus
+ * pinned memory, evicting the least recently used; a plan larger than that on its own is
+ * released when its call returns.  Any pointer may be NULL. */
+int rl_plan_cache_info(int32_t* entries, int64_t* device_bytes, int64_t* pinned_bytes);
 
 /* ------------------------------------------------------------ multi-device
  * rl_optimize over n_dev devices (SURVEY.md §8b device list, §8e): the B instances are
@@ -286,6 +296,13 @@ const char* rl_last_error(void);
 int         rl_abi_version(void);
 /* kernel variant the library would pick for N (samples per lane), or RL_ETOOBIG */
 int         rl_kernel_variant(int32_t N);
+/* the kernel shape of a launch: *K samples per lane (0 = the streaming kernel) and *T lanes
+ * per instance for N samples, a batch of B and mode RL_MODE_MINCURV or RL_MODE_MINTIME on
+ * the calling thread's current device.  Batches that need at most one wave per SIMD in a
+ * latency shape (one instance spread over a CU, 1-4 samples per lane) get it; larger ones
+ * the throughput shapes (4-8 samples per lane).  RL_LAT_SHAPES=0 in the environment keeps
+ * the throughput shapes for every batch.  Returns RL_OK or RL_E*. */
+int         rl_kernel_shape(int32_t N, int32_t B, int32_t mode, int32_t* K, int32_t* T);
 
 #ifdef __cplusplus
 }

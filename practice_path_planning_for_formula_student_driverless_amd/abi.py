@@ -361,6 +361,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_abi_version.restype = C.c_int
     lib.rl_kernel_variant.argtypes = [C.c_int32]
     lib.rl_kernel_variant.restype = C.c_int
+    if hasattr(lib, "rl_kernel_shape"):     # absent only in older experiment builds (A/B bases)
+        lib.rl_kernel_shape.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.rl_kernel_shape.restype = C.c_int
     lib.rl_geom.argtypes = [C.POINTER(RlGeomProblem), C.POINTER(RlCfg), C.c_int32, C.POINTER(C.c_double),
                             C.POINTER(C.c_float)]
     lib.rl_geom.restype = C.c_int
@@ -384,9 +387,24 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         lib.rl_last_call_ms.restype = C.c_int
         lib.rl_release_plan_cache.argtypes = []
         lib.rl_release_plan_cache.restype = C.c_int
+    if hasattr(lib, "rl_last_call_times"):  # absent only in older experiment builds (A/B bases)
+        lib.rl_last_call_times.argtypes = [C.POINTER(C.c_float)] * 4
+        lib.rl_last_call_times.restype = C.c_int
+        lib.rl_plan_cache_info.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        lib.rl_plan_cache_info.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib
     return lib
+
+
+def kernel_shape(N: int, B: int, mode: int) -> tuple:
+    """(K samples per lane, T lanes per instance) librl.so launches for (N, B, mode)."""
+    lib = load_library()
+    k, t = C.c_int32(), C.c_int32()
+    rc = lib.rl_kernel_shape(int(N), int(B), int(mode), C.byref(k), C.byref(t))
+    if rc != RL_OK:
+        raise RuntimeError(f"rl_kernel_shape({N}, {B}, {mode}) = {rc}")
+    return k.value, t.value
 
 
 def cfg_field_names() -> list:

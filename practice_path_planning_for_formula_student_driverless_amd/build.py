@@ -18,8 +18,8 @@ INCLUDE = os.path.join(REPO, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-KERNEL_SRCS = ["csrc/rl_kernels.hip", "csrc/rl_stream.hip", "csrc/rl_geom.hip", "csrc/rl_format.hip", "csrc/rl_abi.cpp"]
-KERNEL_DEPS = KERNEL_SRCS + ["csrc/rl_kernels.h", "csrc/rl_device.h", "csrc/rl_math.h", "csrc/rl_corridor.h"]
+KERNEL_SRCS = ["csrc/rl_kernels.hip", "csrc/rl_kernels_lat.hip", "csrc/rl_stream.hip", "csrc/rl_geom.hip", "csrc/rl_format.hip", "csrc/rl_abi.cpp"]
+KERNEL_DEPS = KERNEL_SRCS + ["csrc/rl_optimize_body.h", "csrc/rl_kernels.h", "csrc/rl_device.h", "csrc/rl_math.h", "csrc/rl_corridor.h"]
 # -ffp-contract=off: HIP defaults to fusing a*b+c into FMA, which would change
 # the reference's roundings.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",

@@ -174,18 +174,17 @@ bool use_stream(int N) {
     return f && f[0] == '1';
 }
 
-// waves of one instance in the kernel launch_optimize / launch_stream picks for N
-int waves_per_instance(int N, bool stream) {
-    if (stream) return 16;                                    // rl_stream.hip: 1024 threads
-    const int k = rl::pick_k(N);
-    if (k <= 0) return 16;
-    const int lanes = (N + k - 1) / k;
-    return (lanes + 63) / 64;
-}
 int device_cus(int dev) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
     return n;
+}
+// waves of one instance in the kernel launch_optimize / launch_stream picks for (N, B, mode)
+int waves_per_instance(int N, int B, bool mintime, bool stream, int cus) {
+    if (stream) return 16;                                    // rl_stream.hip: 1024 threads
+    const rl::Shape s = rl::pick_shape(N, B, mintime, cus);
+    if (s.K <= 0) return 16;
+    return (s.T + 63) / 64;
 }
 
 }  // namespace
@@ -255,6 +254,21 @@ int rl_kernel_variant(int32_t N) {
 }
 
 // cfg::Config defaults, ref:77-113
+// (K, T) the library launches for N samples, a batch of B and `mode` (one of
+// RL_MODE_MINCURV / RL_MODE_MINTIME) on the calling thread's current device
+int rl_kernel_shape(int32_t N, int32_t B, int32_t mode, int32_t* K, int32_t* T) {
+    if (!K || !T || B < 1 || (mode != RL_MODE_MINCURV && mode != RL_MODE_MINTIME))
+        return fail(RL_EINVAL, "rl_kernel_shape: bad argument");
+    if (N < 1 || N > rl::RL_STREAM_MAX_N) return fail(RL_ETOOBIG, "rl_kernel_shape: N out of range");
+    if (use_stream(N)) { *K = 0; *T = 1024; return RL_OK; }   // streaming kernel (samples strided)
+    int dev = 0;
+    const int cus = (hipGetDevice(&dev) == hipSuccess) ? device_cus(dev) : 256;
+    const rl::Shape s = rl::pick_shape(N, B, mode == RL_MODE_MINTIME, cus);
+    *K = s.K;
+    *T = s.T;
+    return RL_OK;
+}
+
 void rl_cfg_default(rl_cfg* c) {
     if (!c) return;
     std::memset(c, 0, sizeof(*c));
@@ -321,9 +335,13 @@ double rl_seed_value(uint64_t seed, int32_t i, double sigma) { return rl::seed_v
 int rl_plan_destroy(rl_plan* plan) {
     if (!plan) return RL_OK;
     hipSetDevice(plan->device);
+    // every stream that may still run a kernel of this plan drains before its buffers go:
+    // a run that failed after queueing the min-time kernel on aux_stream, but before the
+    // run stream waited for it, leaves that kernel reading and writing them
     if (plan->last_stream) hipStreamSynchronize(plan->last_stream);
-    for (void* p : plan->allocs) hipFree(p);
     if (plan->aux_stream) hipStreamSynchronize(plan->aux_stream);
+    if (plan->own_stream) hipStreamSynchronize(plan->own_stream);
+    for (void* p : plan->allocs) hipFree(p);
     for (auto& e : plan->ev)
         if (e) hipEventDestroy(e);
     for (auto& e : plan->ev_end)
@@ -485,8 +503,11 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
     // CU: C4's 512 single-wave instances per track, the drop-in B=1).  Larger batches fill
     // the GPU with either kernel alone and run them one after the other (C3: concurrent
     // 74.2 ms vs 73.1 ms sequential).
+    const int cus = device_cus(p->device);
     const bool both = (p->modes & (RL_MODE_MINCURV | RL_MODE_MINTIME)) == (RL_MODE_MINCURV | RL_MODE_MINTIME) &&
-                      (int64_t)p->B * waves_per_instance(p->N, p->stream) <= (int64_t)8 * device_cus(p->device);
+                      (int64_t)p->B * std::max(waves_per_instance(p->N, p->B, false, p->stream, cus),
+                                               waves_per_instance(p->N, p->B, true, p->stream, cus)) <=
+                          (int64_t)8 * cus;
     if (both) HIPCHK(hipStreamWaitEvent(p->aux_stream, p->ev[0], 0));   // everything queued before the run
     for (int m = 0; m < 2; ++m) {
         if (!(p->modes & (1 << m))) continue;
@@ -908,7 +929,18 @@ int rl_plan_device_outputs(rl_plan* p, int32_t which, rl_out* d) {
 namespace {
 
 constexpr int kCacheEntries = 8;                       // idle plans kept
-constexpr size_t kCacheBytes = (size_t)8 << 30;        // device bytes kept idle
+// device + pinned host bytes kept idle (RL_PLAN_CACHE_MB overrides; 0 disables caching).
+// An entry larger than the budget on its own is not kept either, so one oversized call
+// leaves nothing allocated behind it.
+constexpr size_t kCacheBytesDefault = (size_t)2 << 30;
+size_t cache_budget() {
+    const char* s = std::getenv("RL_PLAN_CACHE_MB");
+    if (!s || !*s) return kCacheBytesDefault;
+    char* end = nullptr;
+    const unsigned long long mb = std::strtoull(s, &end, 10);
+    if (end == s) return kCacheBytesDefault;
+    return (size_t)mb << 20;
+}
 constexpr int kJobEvents = 32;
 
 struct CacheEntry {
@@ -927,7 +959,8 @@ struct CacheEntry {
                segs.size() == k.segs.size() &&
                (segs.empty() || std::memcmp(segs.data(), k.segs.data(), segs.size() * sizeof(double)) == 0);
     }
-    size_t bytes() const { return p ? p->dev_bytes : 0; }
+    // device memory of the plan plus the pinned staging buffer (both stay allocated while idle)
+    size_t bytes() const { return (p ? p->dev_bytes : 0) + pin_bytes; }
 };
 
 void destroy_entry(CacheEntry* e) {
@@ -959,6 +992,7 @@ struct PlanCache {
     }
     void give(CacheEntry* e) {
         std::vector<CacheEntry*> evict;
+        const size_t budget = cache_budget();
         {
             std::lock_guard<std::mutex> g(mu);
             e->tick = ++tick;
@@ -968,7 +1002,9 @@ struct PlanCache {
                 for (CacheEntry* q : idle) t += q->bytes();
                 return t;
             };
-            while (idle.size() > 1 && ((int)idle.size() > kCacheEntries || total() > kCacheBytes)) {
+            // least recently used first, down to the newest entry itself when it alone
+            // exceeds the budget
+            while (!idle.empty() && ((int)idle.size() > kCacheEntries || total() > budget)) {
                 auto lru = std::min_element(idle.begin(), idle.end(),
                                             [](CacheEntry* x, CacheEntry* y) { return x->tick < y->tick; });
                 evict.push_back(*lru);
@@ -976,6 +1012,17 @@ struct PlanCache {
             }
         }
         for (CacheEntry* q : evict) destroy_entry(q);
+    }
+    void info(int32_t* entries, int64_t* dev_bytes, int64_t* pin_bytes) {
+        std::lock_guard<std::mutex> g(mu);
+        int64_t d = 0, h = 0;
+        for (CacheEntry* q : idle) {
+            d += q->p ? (int64_t)q->p->dev_bytes : 0;
+            h += (int64_t)q->pin_bytes;
+        }
+        if (entries) *entries = (int32_t)idle.size();
+        if (dev_bytes) *dev_bytes = d;
+        if (pin_bytes) *pin_bytes = h;
     }
     void clear() {
         std::vector<CacheEntry*> all;
@@ -992,6 +1039,7 @@ PlanCache& plan_cache() {
 }
 
 thread_local float g_last_kernel_ms = -1.0f, g_last_call_ms = -1.0f;
+thread_local float g_last_mode_ms[2] = {-1.0f, -1.0f};    // min-curv / min-time kernel of the last call
 
 int ensure_pinned(CacheEntry* e, size_t bytes) {
     if (bytes <= e->pin_bytes) return RL_OK;
@@ -1046,8 +1094,14 @@ int download_staged(CacheEntry* e, hipStream_t st, const std::vector<CopyJob>& j
     };
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const int nthr = total < ((size_t)8 << 20) ? 1 : (int)std::min<size_t>({8, hw, pieces.size()});
+    // helper threads are an optimisation: if one cannot be started (std::system_error,
+    // std::bad_alloc), the calling thread does its share, and no exception leaves the C ABI
     std::vector<std::thread> th;
-    for (int t = 1; t < nthr; ++t) th.emplace_back(work);
+    try {
+        th.reserve((size_t)std::max(0, nthr - 1));
+        for (int t = 1; t < nthr; ++t) th.emplace_back(work);
+    } catch (...) {
+    }
     work();
     for (auto& t : th) t.join();
     if (bad) return fail(RL_EHIP, "download (staged): event wait failed");
@@ -1066,7 +1120,7 @@ size_t staged_bytes(const std::vector<CopyJob>& jobs) {
 int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
                int32_t modes, const double* centers, const double* Ls, rl_out* out_mc, rl_out* out_mt, float* kms) {
     const auto t0 = std::chrono::steady_clock::now();
-    g_last_kernel_ms = g_last_call_ms = -1.0f;
+    g_last_kernel_ms = g_last_call_ms = g_last_mode_ms[0] = g_last_mode_ms[1] = -1.0f;
     if (int rc = check_inputs(prob, cfg, n_cfg, B, modes, centers)) return rc;
     int ndev = 0, dev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
@@ -1153,6 +1207,8 @@ int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const u
     if (kms) std::memcpy(kms, ms, sizeof(ms));
     pc.give(e);
     g_last_kernel_ms = ms[0];
+    g_last_mode_ms[0] = ms[1];
+    g_last_mode_ms[1] = ms[2];
     g_last_call_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RL_OK;
 }
@@ -1172,6 +1228,20 @@ int rl_last_call_ms(float* kernel_ms, float* call_ms) {
     if (g_last_call_ms < 0.0f) return fail(RL_EINVAL, "no successful rl_optimize / rl_lap_eval on this thread");
     if (kernel_ms) *kernel_ms = g_last_kernel_ms;
     if (call_ms) *call_ms = g_last_call_ms;
+    return RL_OK;
+}
+
+int rl_last_call_times(float* run_ms, float* mincurv_ms, float* mintime_ms, float* call_ms) {
+    if (g_last_call_ms < 0.0f) return fail(RL_EINVAL, "no successful rl_optimize / rl_lap_eval on this thread");
+    if (run_ms) *run_ms = g_last_kernel_ms;
+    if (mincurv_ms) *mincurv_ms = g_last_mode_ms[0];
+    if (mintime_ms) *mintime_ms = g_last_mode_ms[1];
+    if (call_ms) *call_ms = g_last_call_ms;
+    return RL_OK;
+}
+
+int rl_plan_cache_info(int32_t* entries, int64_t* device_bytes, int64_t* pinned_bytes) {
+    plan_cache().info(entries, device_bytes, pinned_bytes);
     return RL_OK;
 }
 
@@ -1255,6 +1325,7 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, 
 // diagnostic builds only: per-phase cycle totals of the last launch (see rl_kernels.hip)
 int rl_debug_stamps(unsigned long long* host, int nblocks) { return rl::debug_stamps(host, nblocks); }
 int rl_debug_stamps_stream(unsigned long long* host, int nblocks) { return rl::debug_stamps_stream(host, nblocks); }
+int rl_debug_stamps_lat(unsigned long long* host, int nblocks) { return rl::debug_stamps_lat(host, nblocks); }
 #endif
 #ifdef RL_COUNT
 // diagnostic builds only: corridor work counters of the stream kernel's translation unit

@@ -35,10 +35,42 @@ constexpr int RL_STREAM_ARRAYS = 15;
 constexpr int RL_REG_MAX_N = 4096;          // register-resident kernel covers N <= 4096
 constexpr int RL_STREAM_MAX_N = 1 << 20;
 
-// samples per lane for N (4 or 8), or -1 if N exceeds the register-resident kernel
+// samples per lane for N (4 or 8) of the throughput shapes, or -1 if N exceeds the
+// register-resident kernel
 int pick_k(int N);
+// (K samples per lane, T lanes per instance) of a register-resident launch
+struct Shape {
+    int K, T;
+};
+// Latency shapes (rl_kernels_lat.hip) by N: one instance spread over a whole CU, for
+// batches that leave most of the GPU idle (build knobs for A/B timing).  Above N = 2048
+// the throughput shape (8, 512) already spreads an instance over 8 waves (a 1024-lane
+// shape would be capped at 128 VGPRs and spill).
+#ifndef RL_LAT1_K
+#define RL_LAT1_K 1      // N <= 256: (1, 256)
+#endif
+#ifndef RL_LAT2_K
+#define RL_LAT2_K 2      // N <= 512: (2, 256)
+#endif
+#ifndef RL_LAT3_K
+#define RL_LAT3_K 2      // N <= 1024: (2, 512)
+#endif
+inline Shape lat_shape(int N) {
+    if (N <= 256) return {RL_LAT1_K, 256 / RL_LAT1_K};
+    if (N <= 512) return {RL_LAT2_K, 512 / RL_LAT2_K};
+    if (N <= 1024) return {RL_LAT3_K, 1024 / RL_LAT3_K};
+    if (N <= 2048) return {4, 512};
+    return {-1, -1};
+}
+// the shape launch_optimize uses for N samples and a batch of B instances on a device with
+// `cus` CUs: the latency shape while B x its waves <= 4 x cus (one wave per SIMD) and
+// RL_LAT_SHAPES is not "0", else the throughput shape; {-1, -1} beyond RL_REG_MAX_N
+Shape pick_shape(int N, int B, bool mintime, int cus);
 // enqueue one persistent launch (one workgroup per instance) on `st`
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
+// the launches of the latency shapes lat_shape(p.N) and of every (4, 512) shape (also the
+// min-time shape for 1024 < N <= 2048 below two instances per CU), rl_kernels_lat.hip
+hipError_t launch_optimize_lat(const KParams& p, bool mintime, hipStream_t st);
 // large-N variant: one 1024-thread workgroup per instance, state in HBM
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st);
 // step 6 geometry (rl_geom.hip): spline knots [5][nk] per axis (s,a,b,c,d), rows [Kmax+dup][9]
@@ -69,6 +101,7 @@ int format_rows(const double* table, int64_t rows, int cols, char* out, uint64_t
 #ifdef RL_STAMPS
 int debug_stamps(unsigned long long* host, int nblocks);
 int debug_stamps_stream(unsigned long long* host, int nblocks);
+int debug_stamps_lat(unsigned long long* host, int nblocks);
 #endif
 #ifdef RL_COUNT
 int debug_counts(unsigned long long* host, int reset);

@@ -730,10 +730,12 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         // iteration is rejected) from one pass over (α, g, lo, hi, coefficients): per
         // step the arithmetic and the per-thread sample order of eval_trial, and
         // block_sum_s reduces each sum on its own, so J and the decrease of every step
-        // are bit-identical to one-at-a-time trials.  Writes nothing.
+        // are bit-identical to one-at-a-time trials.  Writes nothing unless keep0 is set.
         constexpr int MB = RL_BT_BATCH;
         // keep0: step 0 is the first trial of an inner iteration -- also store its α_trial,
-        // q1, q2 and D1α (eval_trial's `keep`), so an accepted first step needs no second pass
+        // q1, q2 and D1α (eval_trial's `keep`) into an_p, Q1, Q2, D1, so an accepted first
+        // step needs no second pass: the accept path skips materialize() for j == 0 and
+        // relies on these writes
         auto eval_trials = [&](const double (&st)[MB], int m, double (&Jn)[MB], double (&dn)[MB], bool keep0) {
             double s3[3 * MB];
 #pragma unroll

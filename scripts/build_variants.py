@@ -34,6 +34,7 @@ VARIANTS = {
     "blk32": {"RL_BLKSZ": 32},
     "nofuse": {"RL_SFUSE": 0},
     "svp0": {"RL_SVP_REG": 0},
+    "lat_k2": {"RL_LAT1_K": 2, "RL_LAT2_K": 4, "RL_LAT3_K": 4},   # (2,128) / (4,128) / (4,256) latency shapes
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }

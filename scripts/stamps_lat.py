@@ -1,0 +1,33 @@
+"""Phase shares of one-instance (drop-in) runs from the RL_STAMPS diagnostic build: the
+latency shape (rl_kernels_lat.hip's stamps) against the throughput shape (RL_LAT_SHAPES=0,
+rl_kernels.hip's stamps; (4, 512) lives in the latency unit).  Shares only: a stamped
+build's absolute time is not the real kernel's."""
+import ctypes as C, os, sys, numpy as np
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "tests"))
+import oracle_lib as O
+from practice_path_planning_for_formula_student_driverless_amd import abi
+lib = abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_stamps.so"))
+names = ["setup", "corridor tail", "mt:κ/vpass/γ", "lin-geom", "PGD loop", "update", "final",
+         "normals + corridor loads", "corridor: inner rays", "corridor: outer rays", "corridor: fallback"]
+for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n2000"):
+    case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)
+    for mode in (1, 2):
+        for thr in (False, True):
+            os.environ["RL_LAT_SHAPES"] = "0" if thr else "1"
+            K, T = abi.kernel_shape(prob.N, 1, mode)
+            h = C.c_void_p(); p = prob.as_c(); arr, n = abi.cfg_array(cfg)
+            assert lib.rl_plan_create(C.byref(h), 0, C.byref(p), arr, n, None, 1, mode) == 0
+            lib.rl_plan_run(h, None)
+            assert lib.rl_plan_run(h, None) == 0
+            ms = C.c_float(); lib.rl_plan_kernel_ms(h, mode, C.byref(ms))
+            st = np.zeros((1, 16), dtype=np.uint64)
+            in_lat = (not thr) or (K, T) == (4, 512)
+            f = lib.rl_debug_stamps_lat if in_lat else lib.rl_debug_stamps
+            assert f(st.ctypes.data_as(C.c_void_p), 1) == 0
+            tot = st.sum(0).astype(float)
+            print(f"{cname} N={prob.N} mode={mode} shape=({K},{T}) kernel {ms.value:.3f} ms (stamped); "
+                  f"wave-0 cycles {tot.sum():.3e}: " +
+                  ", ".join(f"{nm} {100 * tot[i] / tot.sum():.1f}%" for i, nm in enumerate(names) if tot[i] > 0), flush=True)
+            lib.rl_plan_destroy(h)
+os.environ.pop("RL_LAT_SHAPES", None)

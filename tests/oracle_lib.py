@@ -17,7 +17,43 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref_harness.so")
+# the reference built with its README's flags (g++ -std=c++17 -O3), oracle/ref_bench.cpp
+REF_BENCH = os.path.join(ORACLE_DIR, "_ref", "ref_bench_o3")
 GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def write_problem_bin(prob: abi.Problem, cfg: abi.RlCfg, path: str) -> None:
+    """The problem file oracle/ref_bench.cpp reads: int32 N, closed, Ei, Eo; double L,
+    veh_width; rl_cfg; center [N][2], inner [Ei][4], outer [Eo][4] (little endian)."""
+    hdr = np.array([prob.N, 1 if prob.closed else 0, prob.inner_seg.shape[0], prob.outer_seg.shape[0]], dtype="<i4")
+    with open(path, "wb") as f:
+        f.write(hdr.tobytes())
+        f.write(np.array([prob.L, prob.veh_width], dtype="<f8").tobytes())
+        f.write(bytes(cfg))
+        for a in (prob.center, prob.inner_seg, prob.outer_seg):
+            f.write(np.ascontiguousarray(a, dtype="<f8").tobytes())
+
+
+def run_ref_bench(prob: abi.Problem, cfg: abi.RlCfg, mintime: bool, budget_s: float, min_calls: int,
+                  workdir: str) -> dict:
+    """Time the reference's own optimiser (built as its README builds it) on `prob` in a
+    child process on the caller's cores: {"calls", "seconds", "lap", "x0", "ms": [...]}."""
+    import json
+
+    path = os.path.join(workdir, "problem.bin")
+    write_problem_bin(prob, cfg, path)
+    out = subprocess.run([REF_BENCH, path, "mintime" if mintime else "mincurv", str(budget_s), str(min_calls)],
+                         capture_output=True, text=True, check=True).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def ref_bench_build() -> str:
+    """Compiler and flags ref_bench_o3 was built with (oracle/Makefile writes them)."""
+    try:
+        with open(REF_BENCH + ".build") as f:
+            return f.read().strip()
+    except OSError:
+        return ""
 
 _ORACLE = None
 

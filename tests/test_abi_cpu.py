@@ -34,7 +34,9 @@ def test_header_declares_expected_entry_points():
     for must in ("rl_optimize", "rl_plan_create", "rl_plan_run", "rl_plan_fetch", "rl_plan_destroy",
                  "rl_plan_device_outputs", "rl_plan_kernel_ms", "rl_plan_bind_device_outputs", "rl_cfg_default", "rl_cfg_set_mu",
                  "rl_ring_segments", "rl_seed_value", "rl_device_count", "rl_last_error", "rl_abi_version",
-                 "rl_kernel_variant", "rl_geom", "rl_optimize_multi", "rl_lap_eval", "rl_corridor", "rl_format_csv"):
+                 "rl_kernel_variant", "rl_geom", "rl_optimize_multi", "rl_lap_eval", "rl_corridor", "rl_format_csv",
+                 "rl_last_call_ms", "rl_last_call_times", "rl_release_plan_cache", "rl_plan_cache_info",
+                 "rl_kernel_shape"):
         assert must in names
 
 
@@ -114,6 +116,36 @@ def test_kernel_variant_table():
     assert lib.rl_kernel_variant(4097) == 1          # large-N streaming kernel
     assert lib.rl_kernel_variant(10000) == 1
     assert lib.rl_kernel_variant((1 << 20) + 1) == abi.RL_ETOOBIG
+
+
+def test_kernel_shape_table():
+    """Throughput shapes for batches that fill the GPU, latency shapes (one instance over a
+    CU) while the batch needs at most one wave per SIMD in them (256 CUs assumed here)."""
+    MC, MT = abi.RL_MODE_MINCURV, abi.RL_MODE_MINTIME
+    assert abi.kernel_shape(216, 1, MC) == (1, 256)
+    assert abi.kernel_shape(216, 256, MC) == (1, 256)
+    assert abi.kernel_shape(216, 257, MC) == (4, 64)
+    assert abi.kernel_shape(261, 1, MT) == (2, 256)
+    assert abi.kernel_shape(261, 512, MT) == (8, 64)
+    assert abi.kernel_shape(2000, 1, MC) == (4, 512)
+    assert abi.kernel_shape(2000, 1, MT) == (4, 512)
+    assert abi.kernel_shape(1000, 8, MC) == (2, 512)
+    assert abi.kernel_shape(2000, 1024, MC) == (8, 256)
+    assert abi.kernel_shape(2000, 256, MT) == (4, 512)
+    assert abi.kernel_shape(2000, 4096, MT) == (8, 256)
+    assert abi.kernel_shape(4096, 1, MC) == (8, 512)
+    assert abi.kernel_shape(10000, 1, MC) == (0, 1024)
+
+
+def test_plan_cache_queries_without_a_call():
+    """The cache queries touch no device: an empty cache, and no last call on this thread."""
+    lib = abi.load_library()
+    n, d, h = C.c_int32(-1), C.c_int64(-1), C.c_int64(-1)
+    assert lib.rl_plan_cache_info(C.byref(n), C.byref(d), C.byref(h)) == 0
+    if lib.rl_device_count() == 0:
+        assert (n.value, d.value, h.value) == (0, 0, 0)
+        f = C.c_float()
+        assert lib.rl_last_call_times(C.byref(f), None, None, None) == abi.RL_EINVAL
 
 
 def test_compute_fails_loudly_without_gpu():

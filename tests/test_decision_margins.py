@@ -45,6 +45,66 @@ def test_no_decision_within_summation_bound(name, mode):
     assert below == 0 and ratio > 1e3, (name, mode, ratio, n, below)
 
 
+BENCH_REPORT = O.GOLDEN + "/margins_bench.json"
+# every instance of the bench's configurations (bench.py): C2 seeds 0..1023 min-curv, C3
+# seeds 0..4095 both modes, C4 7 tracks x 512 grid points both modes, C5 seeds 0..1023
+BENCH_CONFIGS = {"C2": {"mincurv": 1024}, "C3": {"mincurv": 4096, "mintime": 4096},
+                 "C4": {"mincurv": 3584, "mintime": 3584}, "C5": {"mincurv": 1024, "mintime": 1024}}
+
+
+def _bench_report():
+    import json
+
+    with open(BENCH_REPORT) as f:
+        return json.load(f)
+
+
+def test_bench_configurations_certificate_report():
+    """The committed certificate over the bench's configurations (scripts/margin_report.py):
+    every instance the bench reports has all its Armijo and stop decisions outside the
+    summation-order bound, so the kernels' evals/accepts counters equal the reference's by
+    construction for the whole C2 / C3 / C4 / C5 batches, not only for the instances the
+    GPU tests compare."""
+    rep = _bench_report()
+    for conf, modes in BENCH_CONFIGS.items():
+        for mode, n in modes.items():
+            e = rep[conf][mode]
+            assert e["instances"] == n == len(e["per_instance_min_ratio"]), (conf, mode)
+            assert e["within_bound"] == 0 and e["decisions"] > n, (conf, mode, e["within_bound"])
+            # > 1 is the certificate; the measured minima are 895 (C3 min-curv, seed 3001) and up
+            assert e["min_ratio"] > 100, (conf, mode, e["min_ratio"])
+            assert min(e["per_instance_min_ratio"]) == np.float32(e["min_ratio"]), (conf, mode)
+
+
+def _instance(conf, mode, idx):
+    """(problem, cfg, seed) of instance idx of a bench configuration (margin_report.py order)."""
+    from practice_path_planning_for_formula_student_driverless_amd import distributed as D
+
+    if conf == "C4":
+        t, k = D.c4_items()[idx]
+        case = O.load_case("track_" + D.C4_TRACKS[t])
+        cfg = D.c4_cfgs(O.case_cfg(O.load_case("track_training_map")))[k]
+        return O.case_problem(case), cfg, 0
+    name = {"C2": "cmap1_n2000", "C3": "cmap1_n2000_vp20", "C5": "oval_n10000"}[conf]
+    case = O.load_case(name)
+    return O.case_problem(case), O.case_cfg(case), idx
+
+
+@pytest.mark.parametrize("conf,mode,which", [("C2", "mincurv", "argmin"), ("C2", "mincurv", 777),
+                                             ("C3", "mintime", "argmin"), ("C3", "mincurv", 3000),
+                                             ("C4", "mincurv", "argmin"), ("C4", "mintime", "argmin"),
+                                             ("C4", "mintime", 2047), ("C5", "mincurv", 5)])
+def test_bench_certificate_spot_check(conf, mode, which):
+    """Recompute instances of the committed report (its minimum and others) with the oracle:
+    the same per-instance minimum ratio."""
+    e = _bench_report()[conf][mode]
+    r = np.asarray(e["per_instance_min_ratio"], dtype=np.float32)
+    idx = int(np.argmin(r)) if which == "argmin" else which
+    prob, cfg, seed = _instance(conf, mode, idx)
+    ratio, n, below = margins(prob, cfg, [seed], (mode == "mincurv", mode == "mintime"))
+    assert below == 0 and np.float32(ratio) == r[idx], (conf, mode, idx, ratio, r[idx])
+
+
 def test_margin_report_counts_every_decision():
     # one instance of C2: evals per outer iteration = Armijo tests + 1, accepts = stop tests run
     case = O.load_case("cmap1_n2000")

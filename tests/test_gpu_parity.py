@@ -65,10 +65,23 @@ def compare_outputs(got: abi.Outputs, ref: abi.Outputs, mintime: bool, label: st
 GOLDEN = list(O.manifest()["cases"])    # includes the N=10000 oval (streaming kernel)
 
 
+SHAPES = ["lat", "thr"]     # latency shapes (the default for small batches) / RL_LAT_SHAPES=0
+
+
+def _shapes(monkeypatch, shapes):
+    if shapes == "thr":
+        monkeypatch.setenv("RL_LAT_SHAPES", "0")
+    else:
+        monkeypatch.delenv("RL_LAT_SHAPES", raising=False)
+
+
+@pytest.mark.parametrize("shapes", SHAPES)
 @pytest.mark.parametrize("name", GOLDEN)
-def test_golden_case_vs_reference(name):
-    """seed 0 == the reference: GPU vs the compiled reference's own outputs."""
+def test_golden_case_vs_reference(name, shapes, monkeypatch):
+    """seed 0 == the reference: GPU vs the compiled reference's own outputs, in the
+    latency shape a one-instance call gets and in the throughput shape."""
     _lib_or_skip()
+    _shapes(monkeypatch, shapes)
     case = O.load_case(name)
     meta = case["_meta"]
     prob = O.case_problem(case)
@@ -196,16 +209,20 @@ def _synthetic(N, closed, rng):
                        outer_seg=raceline.edges_for(outer, closed), veh_width=1.0, closed=closed)
 
 
+@pytest.mark.parametrize("shapes", SHAPES)
 @pytest.mark.parametrize("closed", [True, False])
 @pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 8, 63, 64, 65, 255, 256, 257, 392, 512, 1000, 1023, 1025, 1536, 2047,
                                2048, 2049, 3072, 4096])
-def test_ragged_sizes_vs_oracle(N, closed):
-    """Every kernel variant (K,T) and every partial-chunk shape, closed and open.  Open
-    multiples of K take the interior stencils with the boundary selects (rl_kernels.hip
-    OPEN_FAST): one lane holding both ends (4, 8), a single wave with its last active lane
-    inside (392) or at lane 63 (512), and three or more waves per instance (1536, 2048,
-    3072, 4096), whose middle waves hold no boundary sample."""
+def test_ragged_sizes_vs_oracle(N, closed, shapes, monkeypatch):
+    """Every kernel variant (K,T) and every partial-chunk shape, closed and open, in the
+    latency shapes (B = 2: (1, 256), (2, 256), (2, 512), (4, 512); general per-sample
+    stencils for open tracks, K <= 2) and the throughput shapes.  Open multiples of K >= 4
+    take the interior stencils with the boundary selects (rl_optimize_body.h OPEN_FAST):
+    one lane holding both ends (4, 8), a single wave with its last active lane inside (392)
+    or at lane 63 (512), and three or more waves per instance (1536, 2048, 3072, 4096),
+    whose middle waves hold no boundary sample."""
     _lib_or_skip()
+    _shapes(monkeypatch, shapes)
     rng = np.random.default_rng(N)
     prob = _synthetic(N, closed, rng)
     cfg = abi.default_cfg()
@@ -716,6 +733,38 @@ def test_dropin_plan_cache_reuse_is_exact():
             np.testing.assert_array_equal(gmt.v, fmt.v)
 
 
+def test_plan_cache_budget_and_times(monkeypatch):
+    """The plan cache counts device and pinned bytes against its budget: a call whose plan
+    alone exceeds RL_PLAN_CACHE_MB leaves no idle entry (and no memory) behind; within the
+    budget the plan stays cached with its pinned staging, and rl_release_plan_cache frees
+    it.  rl_last_call_times splits the run bracket into the two optimiser kernels."""
+    lib = _lib_or_skip()
+    lib.rl_release_plan_cache()
+    case = O.load_case("track_competition_map2")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+
+    def info():
+        n, d, h = C.c_int32(), C.c_int64(), C.c_int64()
+        assert lib.rl_plan_cache_info(C.byref(n), C.byref(d), C.byref(h)) == 0
+        return n.value, d.value, h.value
+
+    assert info() == (0, 0, 0)
+    monkeypatch.setenv("RL_PLAN_CACHE_MB", "1")          # one instance-batch of 64 exceeds 1 MiB
+    mc_small, _ = raceline.optimize_batch(prob, cfg, np.arange(64, dtype=np.uint64), 64, mintime=False)
+    assert info() == (0, 0, 0)
+    monkeypatch.delenv("RL_PLAN_CACHE_MB")
+    mc, mt = raceline.optimize_batch(prob, cfg, np.arange(64, dtype=np.uint64), 64)
+    n, d, h = info()
+    assert n == 1 and d > 1 << 20 and h > 0
+    run, kmc, kmt, call = (C.c_float() for _ in range(4))
+    assert lib.rl_last_call_times(C.byref(run), C.byref(kmc), C.byref(kmt), C.byref(call)) == 0
+    assert 0 < kmc.value <= run.value * 1.001 and 0 < kmt.value <= run.value * 1.001 and run.value <= call.value
+    for f in abi.OUT_F64 + ("evals", "accepts"):
+        np.testing.assert_array_equal(getattr(mc_small, f), getattr(mc, f), err_msg=f)
+    lib.rl_release_plan_cache()
+    assert info() == (0, 0, 0)
+
+
 def test_empty_plan_reports_kernel_time():
     """N = 0 (ref:689 / 912: an empty Result): the plan runs, and rl_plan_kernel_ms
     reports the empty interval of each mode instead of failing."""
@@ -766,10 +815,10 @@ def test_device_libm_known_answers(tmp_path):
           f"glibc by 1 ulp (glibc misrounds), the rest equal")
 
 
-def test_c4_grid_concurrent_streams_vs_oracle():
-    """C4's schedule (bench.run_c4): one plan per track with per-instance sweep cfgs
-    (mu with a_total_max recomputed, P_max_W, lambda_smooth from distributed.c4_grid), all
-    plans enqueued on concurrent HIP streams before any wait.  Two tracks x 64 grid points
+def test_c4_grid_concurrent_streams_vs_oracle(monkeypatch):
+    """C4's schedule (bench.run_c4): one plan per (track, mode) with per-instance sweep cfgs
+    (mu with a_total_max recomputed, P_max_W, lambda_smooth from distributed.c4_grid), every
+    plan on its own HIP stream, all enqueued before any wait.  Two tracks x 64 grid points
     (every 8th point of the 512-point grid): laps within 1e-4 (measured on the bench's full
     grid: <= 2.4e-8 s), every counter exact."""
     import torch
@@ -777,23 +826,51 @@ def test_c4_grid_concurrent_streams_vs_oracle():
     from practice_path_planning_for_formula_student_driverless_amd import distributed as D
 
     _lib_or_skip()
+    monkeypatch.setenv("RL_LAT_SHAPES", "0")    # the bench's B = 512 shapes at this B = 64
     base = O.case_cfg(O.load_case("track_training_map"))
     cfgs = D.c4_cfgs(base)
     pts = list(range(0, 512, 8))
     plans, probs = [], []
     for t in ("competition_map1", "competition_map_testday3"):
         prob = O.case_problem(O.load_case("track_" + t))
-        plans.append(raceline.Plan(prob, [cfgs[k] for k in pts], B=len(pts),
-                                   modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME))
+        for mode in (abi.RL_MODE_MINCURV, abi.RL_MODE_MINTIME):
+            plans.append(raceline.Plan(prob, [cfgs[k] for k in pts], B=len(pts), modes=mode))
         probs.append(prob)
     streams = [torch.cuda.Stream() for _ in plans]
     for pl, st in zip(plans, streams):
         pl.run(st.cuda_stream)
     for st in streams:
         st.synchronize()
-    for pl, prob in zip(plans, probs):
-        mc, mt = pl.fetch()
-        pl.close()
+    for j, prob in enumerate(probs):
+        mc, _ = plans[2 * j].fetch()
+        _, mt = plans[2 * j + 1].fetch()
         omc, omt = O.run_oracle(prob, [cfgs[k] for k in pts], B=len(pts))
         compare_outputs(mc, omc, False, "c4.mc")
         compare_outputs(mt, omt, True, "c4.mt")
+    for pl in plans:
+        pl.close()
+
+
+@pytest.mark.parametrize("name", [n for n in GOLDEN if n.startswith("track_")] + ["cmap1_n2000"])
+def test_latency_shape_equals_throughput_shape(name, monkeypatch):
+    """The drop-in call (one instance, ref:1347 / 1397) runs a latency shape -- one instance
+    over a CU, 1-4 samples per lane -- and must give the throughput shape's results bit for
+    bit: every column, zero signs and counters; the lap only up to its sum's tree order.
+    Seeds {0, 5} and an accepting cfg sweep point (mu 1.3) exercise different paths."""
+    _lib_or_skip()
+    case = O.load_case(name)
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    cfgs = [cfg, abi.RlCfg.from_dict(cfg.to_dict())]
+    abi.set_mu(cfgs[1], 1.3)
+    got = {}
+    for shapes in SHAPES:
+        _shapes(monkeypatch, shapes)
+        got[shapes] = raceline.optimize_batch(prob, cfgs, [0, 5], 2)
+        k = abi.kernel_shape(prob.N, 2, abi.RL_MODE_MINCURV)[0]
+        assert (k <= 4) if shapes == "lat" else (k >= 4), (shapes, k)
+    for m, (a, b) in enumerate(zip(got["lat"], got["thr"])):
+        for f in abi.OUT_F64 + (("v", "ax", "vpass_sweeps") if m else ()) + ("evals", "accepts"):
+            x, y = getattr(a, f), getattr(b, f)
+            assert np.array_equal(x, y) and np.array_equal(np.signbit(x), np.signbit(y)), f"{name} mode {m}: {f}"
+        if m:
+            np.testing.assert_allclose(a.lap, b.lap, rtol=1e-13, atol=0)
