@@ -20,6 +20,9 @@
  * iteration, v-pass sweeps that changed something) and the build-defined
  * alpha seeds of SURVEY.md §8d (seed 0 == the reference exactly).
  */
+#ifndef ORACLE_FMA
+#define ORACLE_FMA 0   /* 1: liboracle_fma.so, the checker of the RL_FMA kernel build */
+#endif
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -269,7 +272,12 @@ static double cost_grad(const Ops* o, const double* A1, const double* A2, const 
     int N = o->N;
     D1(o, alpha, w->a1);
     D2(o, alpha, w->a2);
+#if ORACLE_FMA
+    /* the contracted evaluation of the RL_FMA kernels (checker of that build only) */
+    for (int i = 0; i < N; ++i) w->r[i] = W[i] * fma(A2[i], w->a2[i], fma(A1[i], w->a1[i], N0[i]));
+#else
     for (int i = 0; i < N; ++i) w->r[i] = W[i] * (N0[i] + A1[i] * w->a1[i] + A2[i] * w->a2[i]);
+#endif
     double J = 0;
     if (gamma2) { for (int i = 0; i < N; ++i) J += gamma2[i] * w->r[i] * w->r[i]; }
     else { for (int i = 0; i < N; ++i) J += w->r[i] * w->r[i]; }
@@ -285,7 +293,11 @@ static double cost_grad(const Ops* o, const double* A1, const double* A2, const 
     D2T(o, w->q2, w->g2);
     D1(o, alpha, w->D1a);
     D1T(o, w->D1a, w->gsm);
+#if ORACLE_FMA
+    for (int i = 0; i < N; ++i) grad[i] = fma(2.0 * lambda, w->gsm[i], 2.0 * (w->g1[i] + w->g2[i]));
+#else
     for (int i = 0; i < N; ++i) grad[i] = 2.0 * (w->g1[i] + w->g2[i]) + 2.0 * lambda * w->gsm[i];
+#endif
     return J;
 }
 
@@ -471,7 +483,11 @@ static void run_instance(const rl_problem* pr, const rl_cfg* C, uint64_t seed, i
             int accepted = 0, bt = 0;
             while (bt < 20) {
                 for (int i = 0; i < N; ++i) {
+#if ORACLE_FMA
+                    double ai = fma(-step, s->grad[i], s->alpha[i]);
+#else
                     double ai = s->alpha[i] - step * s->grad[i];
+#endif
                     s->anew[i] = smin(s->hi[i], smax(s->lo[i], ai));
                 }
                 double Jn = cost_grad(&o, s->A1, s->A2, s->N0, s->W, g2w, C->lambda_smooth, s->anew, s->gnew, &s->w,

@@ -15,6 +15,9 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "_lib", "librl.so")
+# experiment builds only (scripts/build_variants.py): RL_LIB names another librl.so to load
+if os.environ.get("RL_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["RL_LIB"])
 
 RL_OK = 0
 RL_EINVAL = -1

@@ -134,7 +134,7 @@ RingHost make_ring(const double* s, int E) {
     }
     // fp32 copies for the side filter (rl_corridor.h ring_rays): vertices, then block
     // circles with the radius rounded up; packed after the fp64 circles
-    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M, 0.0f);
+    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M + (size_t)4 * nb, 0.0f);
     for (int v = 0; v < 2 * R.M; ++v) f32[v] = (float)R.vtx[v];
     for (int b = 0; b < nb; ++b) {
         float* o = &f32[(size_t)2 * R.M + (size_t)4 * b];
@@ -153,6 +153,34 @@ RingHost make_ring(const double* s, int E) {
         float hf = (float)hr;
         if ((double)hf < hr) hf = std::nextafter(hf, INFINITY);
         o[2] = hf;
+    }
+    // Direction cone per block (rl_corridor.h RL_ALONG): the smallest arc (mod pi) holding the
+    // directions of the segments that end in the block, as its unit centre (dx, dy) and
+    // s = sin(half width + 1e-3) + 1e-5 (fp32 evaluation margin); s = 2 (never "well
+    // conditioned") for an arc wider than pi/2 - 1e-3, a zero-length or non-finite segment
+    for (int b = 0; b < nb; ++b) {
+        float* o = &f32[(size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M + (size_t)4 * b];
+        std::vector<double> ang;
+        bool ok = true;
+        for (int v = b * rl::RL_BLK; v < (b + 1) * rl::RL_BLK; ++v) {
+            if (!ends[v]) continue;
+            const double vx = R.rec[v].vx, vy = R.rec[v].vy;
+            if (!std::isfinite(vx) || !std::isfinite(vy) || (vx == 0.0 && vy == 0.0)) { ok = false; break; }
+            double a = std::atan2(vy, vx);
+            a = std::fmod(a + 2 * M_PI, M_PI);
+            ang.push_back(a);
+        }
+        o[0] = 1.0f; o[1] = 0.0f; o[2] = 2.0f; o[3] = 0.0f;
+        if (!ok || ang.empty()) continue;
+        std::sort(ang.begin(), ang.end());
+        double gap = ang.front() + M_PI - ang.back(), start = ang.front();   // the wrap-around gap
+        for (size_t j = 1; j < ang.size(); ++j)
+            if (ang[j] - ang[j - 1] > gap) { gap = ang[j] - ang[j - 1]; start = ang[j]; }
+        const double half = 0.5 * (M_PI - gap), mid = start + half;
+        if (!(half + 1e-3 < 0.5 * M_PI - 1e-6)) continue;
+        o[0] = (float)std::cos(mid);
+        o[1] = (float)std::sin(mid);
+        o[2] = (float)(std::sin(half + 1e-3) + 1e-5);
     }
     const size_t n64 = R.blk.size();
     R.blk.resize(rl::ring_blk_doubles((size_t)R.M), 0.0);

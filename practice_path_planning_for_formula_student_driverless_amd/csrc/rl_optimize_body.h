@@ -439,6 +439,32 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
     };
 
+    // ---- ghost samples (latency shapes: K <= 2 samples per lane, several waves) ----
+    // Each thread keeps the PGD state of its chunk's two neighbour samples (base-1 and
+    // base+cnt): α, gradient and corridor bounds.  A trial's neighbour values are then its
+    // own projections of them (select forms, the reference's std::min/std::max, which the
+    // owner's maxNum/minNum forms equal bit for bit), so the trial needs no exchange and no
+    // barrier; after an accepted step each thread recomputes the neighbours' gradients
+    // from the q1, q2, D1α the evaluation left in LDS (every sample's, double-buffered by
+    // the parity of the evaluation's one barrier), with the same expressions the owners
+    // use.  One barrier per evaluation instead of two: in a one-instance launch the
+    // barrier and its LDS round trip, not the arithmetic, set the latency.
+#ifndef RL_GHOST
+#define RL_GHOST 1
+#endif
+    constexpr bool GHOST = RL_GHOST && NW > 1 && K <= 2;
+    constexpr int KT = K * T;
+    __shared__ double gq[GHOST ? 2 * 3 * KT : 1];      // [parity][q1 | q2 | D1α][sample]
+    __shared__ double gred[GHOST ? 2 * 2 * NW : 1];    // [parity][J | decrease][wave]
+    auto wrapj = [&](int j) RL_AI -> int {
+        if (CLOSED) { j %= N; return j < 0 ? j + N : j; }
+        return j < 0 ? 0 : (j >= N ? N - 1 : j);      // open: the boundary forms read none of these
+    };
+    const int jl2 = wrapj(base - 2), jl1 = wrapj(base - 1), jr1 = wrapj(base + cnt), jr2 = wrapj(base + cnt + 1);
+    double cL = 0.0, gL = 0.0, loL = 0.0, hiL = 0.0, tL = 0.0;   // sample base-1
+    double cR = 0.0, gR = 0.0, loR = 0.0, hiR = 0.0, tR = 0.0;   // sample base+cnt
+    int gpar = 0, gpar_last = 0;
+
     // ---- P-neighbourhood helpers --------------------------------------------
     // P with a halo of 2 on each side: px[j] = P[base-2+j] (wrapped / clamped)
     auto loadP = [&](double (&px)[K + 4], double (&py)[K + 4]) RL_AI {
@@ -553,6 +579,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             const double2 v = bnd[k * T + tid];
             lo[k] = (k < cnt) ? v.x : 0.0;
             hi[k] = (k < cnt) ? v.y : 0.0;
+        }
+        if constexpr (GHOST) {                                // the neighbour samples' bounds
+            const double2 vl = bnd[(jl1 % K) * T + jl1 / K], vr = bnd[(jr1 % K) * T + jr1 / K];
+            loL = vl.x; hiL = vl.y; loR = vr.x; hiR = vr.y;
         }
         __syncthreads();      // the area is written again (v-pass relaxation, coefficients)
     };
@@ -843,10 +873,17 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 for (int k = 0; k < K; ++k) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
             }
         }
-        xpub(0, a);
-        if constexpr (NW > 1) __syncthreads();
         double lv, rv;
-        xget(0, a, lv, rv);
+        if constexpr (GHOST) {               // the neighbours' values of a: no exchange
+            lv = trial ? tL : cL;
+            rv = trial ? tR : cR;
+        } else {
+            xpub(0, a);
+#ifndef RL_PROBE_NOB1       // timing probe only (wrong results): the trial halo's barrier removed
+            if constexpr (NW > 1) __syncthreads();
+#endif
+            xget(0, a, lv, rv);
+        }
         fill_pad(a, rv);
         double pJ = 0.0, pJsm = 0.0;
         double jr[K];
@@ -893,13 +930,32 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             for (int k = 0; k < K; ++k) acc(k);
         }
         pJ = __builtin_fma(lam_act, pJsm, pJ);         // J += λ·Jsm (ref:663 / 883), per lane
-        xpub(1, q1);
-        xpub(2, q2);
-        xpub(3, a1v);
+        if constexpr (GHOST) {
+            double* const Q = &gq[gpar * 3 * KT];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k < cnt) { Q[base + k] = q1[k]; Q[KT + base + k] = q2[k]; Q[2 * KT + base + k] = a1v[k]; }
+        } else {
+            xpub(1, q1);
+            xpub(2, q2);
+            xpub(3, a1v);
+        }
         const double z = wave_sum_xy(pJ, pdec, lane & 1);   // lane 0: Σ J terms, lane 1: Σ decrease
         if constexpr (NW == 1) {             // the wave sums are the block sums
             dec = readlane(z, 1);
             return readlane(z, 0);
+        }
+        if constexpr (GHOST) {               // double-buffered: the only barrier of the evaluation
+            double* const R = &gred[gpar * 2 * NW];
+            if (lane < 2) R[lane * NW + wid] = z;
+            __syncthreads();
+            double J = R[0], D = R[NW];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) { J += R[w]; D += R[NW + w]; }
+            dec = D;
+            gpar_last = gpar;
+            gpar ^= 1;
+            return J;
         }
         if (lane < 2) sm.red[lane][wid] = z;
         __syncthreads();
@@ -912,9 +968,20 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // gradient of the last evaluation (ref:668-673 / 886-893)
     auto eval_grad = [&](double (&g)[K]) RL_AI {
         double l1, r1, l2, r2, l3, r3;
-        xget(1, q1, l1, r1);
-        xget(2, q2, l2, r2);
-        xget(3, a1v, l3, r3);
+        if constexpr (GHOST) {
+            const double* const Q = &gq[gpar_last * 3 * KT];
+            l1 = Q[jl1]; r1 = Q[jr1]; l2 = Q[KT + jl1]; r2 = Q[KT + jr1]; l3 = Q[2 * KT + jl1]; r3 = Q[2 * KT + jr1];
+            // the neighbour samples' gradients (the owners' expressions, index base-1 / base+cnt)
+            const double q1a = (!RAGGED || cnt == K) ? q1[K - 1] : pick(q1, cnt > 0 ? cnt - 1 : 0);
+            const double q2a = (!RAGGED || cnt == K) ? q2[K - 1] : pick(q2, cnt > 0 ? cnt - 1 : 0);
+            const double a1a = (!RAGGED || cnt == K) ? a1v[K - 1] : pick(a1v, cnt > 0 ? cnt - 1 : 0);
+            gL = grad_at(-1, Q[jl2], l1, q1[0], Q[KT + jl2], l2, q2[0], Q[2 * KT + jl2], l3, a1v[0]);
+            gR = grad_at(cnt, q1a, r1, Q[jr2], q2a, r2, Q[KT + jr2], a1a, r3, Q[2 * KT + jr2]);
+        } else {
+            xget(1, q1, l1, r1);
+            xget(2, q2, l2, r2);
+            xget(3, a1v, l3, r3);
+        }
         fill_pad(q1, r1);
         fill_pad(q2, r2);
         fill_pad(a1v, r3);
@@ -998,6 +1065,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) { al[k] = 0.0; gr[k] = 0.0; }   // ref:757 / 1041
+        cL = cR = gL = gR = 0.0;
         __syncthreads();
         RL_STAMP(5);
         if (outer < MO) {
@@ -1015,6 +1083,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     // loop, where they would hold 2K VGPRs for the whole kernel)
                     double s0 = seed_value(seed, opaque(base) + k, RL_SEED_SIGMA);
                     al[k] = (k < cnt) ? smin(hi[k], smax(lo[k], s0)) : 0.0;
+                }
+                if constexpr (GHOST) {
+                    cL = smin(hiL, smax(loL, seed_value(seed, jl1, RL_SEED_SIGMA)));
+                    cR = smin(hiR, smax(loR, seed_value(seed, jr1, RL_SEED_SIGMA)));
                 }
             }
         }
@@ -1164,6 +1236,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #pragma unroll
                 for (int k = 0; k < K; ++k) nxt[k] = smin(hi[k], smax(lo[k], ai[k]));   // the select forms
             }
+            if constexpr (GHOST) {               // the neighbour samples' trial values
+                tL = smin(hiL, smax(loL, cL - step * gL));
+                tR = smin(hiR, smax(loR, cR - step * gR));
+            }
         };
         double dec;
         double J = eval_j(al, al, gr, false, dec);
@@ -1185,6 +1261,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 ++evals;
                 if (Jn <= J + armijo_c * dec) {
                     eval_grad(g);
+                    if constexpr (GHOST) { cL = tL; cR = tR; }
                     J = Jn;
                     ++accepts;
                     break;

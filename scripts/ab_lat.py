@@ -10,8 +10,10 @@ import oracle_lib as O
 from practice_path_planning_for_formula_student_driverless_amd import abi
 
 libs = {"base": abi.load_library()}
-for p in sorted(glob.glob(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_lat*.so"))):
-    libs[os.path.basename(p)[6:-3]] = abi.load_library(p)
+for p in sorted(glob.glob(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_*.so"))):
+    n = os.path.basename(p)[6:-3]
+    if not (n in ("stamps", "count") or n.startswith("probe")):
+        libs[n] = abi.load_library(p)
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 CASES = ["track_training_map", "track_competition_map_testday3", "cmap1_n2000"]
 res = {}

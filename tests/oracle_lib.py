@@ -55,45 +55,59 @@ def ref_bench_build() -> str:
     except OSError:
         return ""
 
+
+ORACLE_FMA_SO = os.path.join(ORACLE_DIR, "liboracle_fma.so")   # checker of the RL_FMA kernel build
 _ORACLE = None
+_ORACLE_FMA = None
 
 
 def build_oracle() -> None:
-    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so"], check=True)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so", "liboracle_fma.so"], check=True)
 
 
-def oracle() -> C.CDLL:
-    global _ORACLE
+def oracle(fma: bool = False) -> C.CDLL:
+    """The C restatement; fma=True: its contracted variant (oracle/Makefile liboracle_fma.so),
+    the checker of a librl.so built with RL_FMA=1."""
+    global _ORACLE, _ORACLE_FMA
+    if fma:
+        if _ORACLE_FMA is None:
+            if not os.path.exists(ORACLE_FMA_SO):
+                build_oracle()
+            _ORACLE_FMA = _declare(C.CDLL(ORACLE_FMA_SO))
+        return _ORACLE_FMA
     if _ORACLE is None:
         if not os.path.exists(ORACLE_SO):
             build_oracle()
-        lib = C.CDLL(ORACLE_SO)
-        abi.declare_optimize(lib.oracle_optimize)
-        lib.oracle_optimize_range.restype = C.c_int
-        lib.oracle_optimize_range.argtypes = [C.POINTER(abi.RlProblem), C.POINTER(abi.RlCfg), C.c_int32,
-                                              C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_int32,
-                                              C.POINTER(abi.RlOut), C.POINTER(abi.RlOut)]
-        lib.oracle_cfg_default.argtypes = [C.POINTER(abi.RlCfg)]
-        lib.oracle_seed_value.argtypes = [C.c_uint64, C.c_int32, C.c_double]
-        lib.oracle_seed_value.restype = C.c_double
-        lib.oracle_vpass.argtypes = [C.POINTER(abi.RlCfg), C.POINTER(C.c_double), C.c_int, C.c_double, C.c_int,
-                                     C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32)]
-        lib.oracle_vpass.restype = C.c_double
-        lib.oracle_margin_reset.argtypes = []
-        lib.oracle_margin_reset.restype = None
-        lib.oracle_margin_get.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
-        lib.oracle_margin_get.restype = None
-        lib.oracle_ring_segments.argtypes = [C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_double)]
-        lib.oracle_ring_segments.restype = C.c_int
-        lib.oracle_geom.argtypes = [C.POINTER(abi.RlGeomProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double)]
-        lib.oracle_geom.restype = C.c_int
-        lib.oracle_corridor.argtypes = [C.POINTER(abi.RlProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double),
-                                        C.POINTER(C.c_double)]
-        lib.oracle_corridor.restype = C.c_int
-        lib.oracle_format_rows.argtypes = [C.POINTER(C.c_double), C.c_longlong, C.c_int, C.c_char_p, C.c_longlong]
-        lib.oracle_format_rows.restype = C.c_longlong
-        _ORACLE = lib
+        _ORACLE = _declare(C.CDLL(ORACLE_SO))
     return _ORACLE
+
+
+def _declare(lib: C.CDLL) -> C.CDLL:
+    abi.declare_optimize(lib.oracle_optimize)
+    lib.oracle_optimize_range.restype = C.c_int
+    lib.oracle_optimize_range.argtypes = [C.POINTER(abi.RlProblem), C.POINTER(abi.RlCfg), C.c_int32,
+                                          C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_int32,
+                                          C.POINTER(abi.RlOut), C.POINTER(abi.RlOut)]
+    lib.oracle_cfg_default.argtypes = [C.POINTER(abi.RlCfg)]
+    lib.oracle_seed_value.argtypes = [C.c_uint64, C.c_int32, C.c_double]
+    lib.oracle_seed_value.restype = C.c_double
+    lib.oracle_vpass.argtypes = [C.POINTER(abi.RlCfg), C.POINTER(C.c_double), C.c_int, C.c_double, C.c_int,
+                                 C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32)]
+    lib.oracle_vpass.restype = C.c_double
+    lib.oracle_margin_reset.argtypes = []
+    lib.oracle_margin_reset.restype = None
+    lib.oracle_margin_get.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    lib.oracle_margin_get.restype = None
+    lib.oracle_ring_segments.argtypes = [C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_double)]
+    lib.oracle_ring_segments.restype = C.c_int
+    lib.oracle_geom.argtypes = [C.POINTER(abi.RlGeomProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double)]
+    lib.oracle_geom.restype = C.c_int
+    lib.oracle_corridor.argtypes = [C.POINTER(abi.RlProblem), C.POINTER(abi.RlCfg), C.POINTER(C.c_double),
+                                    C.POINTER(C.c_double)]
+    lib.oracle_corridor.restype = C.c_int
+    lib.oracle_format_rows.argtypes = [C.POINTER(C.c_double), C.c_longlong, C.c_int, C.c_char_p, C.c_longlong]
+    lib.oracle_format_rows.restype = C.c_longlong
+    return lib
 
 
 def oracle_cfg_default() -> abi.RlCfg:
@@ -109,8 +123,9 @@ def ring_segments(ring: np.ndarray, closed: bool) -> np.ndarray:
     return seg[:n].copy()
 
 
-def run_oracle(prob: abi.Problem, cfgs, seeds=None, B: int = 1, modes=(True, True), b_range=None):
-    """Run the C oracle.  Returns (Outputs|None for min-curv, Outputs|None for min-time)."""
+def run_oracle(prob: abi.Problem, cfgs, seeds=None, B: int = 1, modes=(True, True), b_range=None, fma=False):
+    """Run the C oracle (fma: its contracted variant).  Returns (Outputs|None for min-curv,
+    Outputs|None for min-time)."""
     cfg_arr, ncfg = abi.cfg_array(cfgs)
     mo = int(cfg_arr[0].max_outer_iters)
     seeds_a = abi.seed_array(seeds)
@@ -120,7 +135,7 @@ def run_oracle(prob: abi.Problem, cfgs, seeds=None, B: int = 1, modes=(True, Tru
     c_mt = out_mt.as_c() if out_mt else None
     p = prob.as_c()
     b0, b1 = b_range if b_range else (0, B)
-    rc = oracle().oracle_optimize_range(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B, b0, b1,
+    rc = oracle(fma).oracle_optimize_range(C.byref(p), cfg_arr, ncfg, abi.u64ptr(seeds_a), B, b0, b1,
                                         C.byref(c_mc) if c_mc else None, C.byref(c_mt) if c_mt else None)
     if rc != 0:
         raise RuntimeError(f"oracle_optimize failed rc={rc}")

@@ -616,6 +616,34 @@ def _corridor_cases():
     outer = np.stack([center[sel, 0] + 1.7 * nx[sel], center[sel, 1] + 1.7 * ny[sel]], axis=1)
     out.append(("vertex_rays_far", abi.Problem(center=center, L=1.0, inner_seg=raceline.ring_edges(inner),
                                                outer_seg=raceline.ring_edges(outer), veh_width=0.6, closed=True)))
+    # segments nearly parallel to sample rays, near and far along them (along-ray culling,
+    # rl_corridor.h RL_ALONG: the computed t of such a pair is ill conditioned, so its block
+    # must not be culled by the circle's distance along the ray): spikes of the outer ring
+    # lying on (or within 1e-14 .. 1e-3 rad of) the normal ray of every 7th sample, starting
+    # 0.5 m to 40 m out, plus spikes on the far side of the track behind the inner ring
+    N = 420
+    t = np.linspace(0, 2 * np.pi, N, endpoint=False)
+    center = np.stack([26 * np.cos(t) + 3 * np.cos(2 * t), 17 * np.sin(t)], axis=1)
+    tx = (np.roll(center[:, 0], -1) - np.roll(center[:, 0], 1)) * 0.5
+    ty = (np.roll(center[:, 1], -1) - np.roll(center[:, 1], 1)) * 0.5
+    nn = np.sqrt(tx * tx + ty * ty)
+    nx, ny = -ty / nn, tx / nn
+    k = np.linspace(0, 2 * np.pi, 131, endpoint=False)
+    inner = np.stack([23 * np.cos(k) + 3 * np.cos(2 * k), 14.2 * np.sin(k)], axis=1)
+    outer = np.stack([29 * np.cos(k) + 3 * np.cos(2 * k), 19.8 * np.sin(k)], axis=1)
+    spikes = []
+    tilts = [0.0, 1e-14, 1e-12, 1e-9, 1e-6, 1e-4, 9e-4, 2e-3, 1e-2]
+    for j, i in enumerate(range(0, N, 7)):
+        tilt, d0 = tilts[j % len(tilts)], [0.5, 3.0, 12.0, 40.0][j % 4]
+        for sgn in (1.0, -1.0):
+            ux, uy = sgn * nx[i], sgn * ny[i]
+            a = np.array([center[i, 0] + d0 * ux, center[i, 1] + d0 * uy])
+            c, s_ = np.cos(tilt), np.sin(tilt)
+            b = a + 6.0 * np.array([c * ux - s_ * uy, s_ * ux + c * uy])
+            spikes.append([a[0], a[1], b[0], b[1]])
+    out.append(("near_parallel_spikes", abi.Problem(
+        center=center, L=1.0, inner_seg=raceline.ring_edges(inner),
+        outer_seg=np.vstack([raceline.ring_edges(outer), np.array(spikes)]), veh_width=0.6, closed=True)))
     # a NaN ring coordinate (either sign bit): the side filter takes every pair of that
     # ring as a candidate, and the exact expressions ignore the NaN segments like the
     # reference's (no hit, std::min keeps the running minimum)

@@ -6,6 +6,8 @@ Also the known answers the reference's data holds: the oracle's
 cfg defaults equal cfg::Config's, the error path and the order-invariance of
 the shuffled cone files are recorded in the manifest.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -198,3 +200,20 @@ def test_oracle_format_rows_matches_reference_csv():
     case = O.load_geom_case("training_map")
     body = case["_csv"].split(b"\n", 1)[1]
     assert O.oracle_format_rows(case["rows"]) == body
+
+
+@pytest.mark.skipif(not os.path.exists(O.REF_BENCH), reason="oracle/_ref/ref_bench_o3 is built from /root/reference "
+                                                             "(build container only)")
+@pytest.mark.parametrize("name,mintime", [("track_training_map", False), ("track_training_map", True),
+                                          ("cmap1_n2000", False)])
+def test_ref_bench_o3_reproduces_fixtures(name, mintime, tmp_path):
+    """The CPU baseline binary (the reference built with its README's g++ -std=c++17 -O3,
+    oracle/ref_bench.cpp) computes what the fixtures hold: the timed calls are the real ones."""
+    case = O.load_case(name)
+    r = O.run_ref_bench(O.case_problem(case), O.case_cfg(case), mintime, 0.0, 1, str(tmp_path))
+    assert r["calls"] == 1 and len(r["ms"]) == 1
+    pre = "mt" if mintime else "mc"
+    assert r["x0"] == float(case[f"{pre}_x"][0])
+    if mintime:
+        assert r["lap"] == float(case["mt_lap"])
+    assert O.ref_bench_build().endswith("-std=c++17 -O3")
