@@ -35,6 +35,8 @@ VARIANTS = {
     "nofuse": {"RL_SFUSE": 0},
     "svp0": {"RL_SVP_REG": 0},
     "lat_k2": {"RL_LAT1_K": 2, "RL_LAT2_K": 4, "RL_LAT3_K": 4},   # (2,128) / (4,128) / (4,256) latency shapes
+    "lat1k2": {"RL_LAT1_K": 2},          # (2,128) for N <= 256 (ghost samples at K = 2)
+    "lat2k1": {"RL_LAT2_K": 1},          # (1,512) for 256 < N <= 512 (8 waves, one sample per lane)
     "probe_nob1": {"RL_PROBE_NOB1": 1},
     "ghost0": {"RL_GHOST": 0},
     "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)           # latency shapes with the two-barrier evaluation (A/B of the ghost samples)  # timing probe (wrong results): scripts/probe_lat.py
