@@ -50,7 +50,7 @@ struct Shape {
 #define RL_LAT1_K 1      // N <= 256: (1, 256)
 #endif
 #ifndef RL_LAT2_K
-#define RL_LAT2_K 2      // N <= 512: (2, 256)
+#define RL_LAT2_K 1      // N <= 512: (1, 512), 8 waves (A/B: testday3 N=261 2.20 -> 1.75 ms vs (2, 256))
 #endif
 #ifndef RL_LAT3_K
 #define RL_LAT3_K 2      // N <= 1024: (2, 512)

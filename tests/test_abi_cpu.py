@@ -125,7 +125,9 @@ def test_kernel_shape_table():
     assert abi.kernel_shape(216, 1, MC) == (1, 256)
     assert abi.kernel_shape(216, 256, MC) == (1, 256)
     assert abi.kernel_shape(216, 257, MC) == (4, 64)
-    assert abi.kernel_shape(261, 1, MT) == (2, 256)
+    assert abi.kernel_shape(261, 1, MT) == (1, 512)
+    assert abi.kernel_shape(261, 128, MC) == (1, 512)
+    assert abi.kernel_shape(261, 129, MC) == (8, 64)
     assert abi.kernel_shape(261, 512, MT) == (8, 64)
     assert abi.kernel_shape(2000, 1, MC) == (4, 512)
     assert abi.kernel_shape(2000, 1, MT) == (4, 512)
