@@ -62,7 +62,9 @@ DROPIN_CASES = ["track_" + t for t in D.C4_TRACKS] + ["cmap1_n2000"]
 def source_sha() -> str:
     """Hash of the kernel sources: a PMC summary is used only if measured on this code."""
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(PKG, "csrc", "*"))) + [os.path.join(REPO, "include", "rl_abi.h")]
+    # (build.py too: its per-source compiler flags change the code)
+    files = sorted(glob.glob(os.path.join(PKG, "csrc", "*"))) + [os.path.join(REPO, "include", "rl_abi.h"),
+                                                                 os.path.join(PKG, "build.py")]
     for f in files:
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())

@@ -18,12 +18,19 @@ INCLUDE = os.path.join(REPO, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-KERNEL_SRCS = ["csrc/rl_kernels.hip", "csrc/rl_kernels_lat.hip", "csrc/rl_stream.hip", "csrc/rl_geom.hip", "csrc/rl_format.hip", "csrc/rl_abi.cpp"]
+KERNEL_SRCS = ["csrc/rl_kernels.hip", "csrc/rl_kernels_lat.hip", "csrc/rl_kernels_mid.hip", "csrc/rl_stream.hip", "csrc/rl_geom.hip", "csrc/rl_format.hip", "csrc/rl_abi.cpp"]
 KERNEL_DEPS = KERNEL_SRCS + ["csrc/rl_optimize_body.h", "csrc/rl_kernels.h", "csrc/rl_device.h", "csrc/rl_math.h", "csrc/rl_corridor.h"]
 # -ffp-contract=off: HIP defaults to fusing a*b+c into FMA, which would change
 # the reference's roundings.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
              "-I" + INCLUDE, "-Wno-unused-command-line-argument"]
+# per-source extra flags of the product build: the latency shapes run one wave per SIMD,
+# where nothing hides a dependent instruction's latency but the wave's own independent
+# instructions, so their translation units use LLVM's ILP-oriented schedulers (A/B,
+# B=1 training_map min-curv 1.43 -> 1.32 ms, C3 min-time 4.73 -> 4.32 ms;
+# the throughput and streaming kernels were slower under them)
+TU_FLAGS = {"csrc/rl_kernels_lat.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+            "csrc/rl_kernels_mid.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 
 def _stale(target: str, deps) -> bool:
@@ -50,15 +57,18 @@ def build_lib(force: bool = False) -> str:
     return out
 
 
-def _compile_link(srcs, flags, out, objdir) -> None:
+def _compile_link(srcs, flags, out, objdir, tu_flags=None) -> None:
     """One hipcc process per translation unit (in parallel), then one link: the
-    kernel file alone takes ~100 s, so the others compile beside it."""
+    kernel file alone takes ~100 s, so the others compile beside it.  tu_flags:
+    extra flags per source (TU_FLAGS by default)."""
+    tu_flags = TU_FLAGS if tu_flags is None else tu_flags
     from concurrent.futures import ThreadPoolExecutor
 
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
     with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
-        for f in [ex.submit(_run, [HIPCC, *HIP_FLAGS, *flags, "-c", s, "-o", o], PKG) for s, o in zip(srcs, objs)]:
+        for f in [ex.submit(_run, [HIPCC, *HIP_FLAGS, *flags, *tu_flags.get(s, []), "-c", s, "-o", o], PKG)
+                  for s, o in zip(srcs, objs)]:
             f.result()
     tmp = out + ".tmp"
     _run([HIPCC, *HIP_FLAGS, "-shared", *objs, "-o", tmp], cwd=PKG)
@@ -66,12 +76,15 @@ def _compile_link(srcs, flags, out, objdir) -> None:
 
 
 def build_variant(name: str, defines: dict) -> str:
-    """Experiment build: _lib/variants/librl_<name>.so with -D overrides (A/B timing only)."""
+    """Experiment build: _lib/variants/librl_<name>.so with -D overrides (A/B timing only);
+    a "_tu" entry maps sources to their extra flags (replacing those sources' TU_FLAGS)."""
+    defines = dict(defines)
+    tu = {**TU_FLAGS, **defines.pop("_tu", {})}
     vdir = os.path.join(LIB_DIR, "variants")
     os.makedirs(vdir, exist_ok=True)
     out = os.path.join(vdir, f"librl_{name}.so")
     flags = [f"-D{k}={v}" for k, v in defines.items()]
-    _compile_link(KERNEL_SRCS, flags, out, os.path.join(vdir, "obj_" + name))
+    _compile_link(KERNEL_SRCS, flags, out, os.path.join(vdir, "obj_" + name), tu)
     return out
 
 

@@ -1354,6 +1354,7 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, 
 int rl_debug_stamps(unsigned long long* host, int nblocks) { return rl::debug_stamps(host, nblocks); }
 int rl_debug_stamps_stream(unsigned long long* host, int nblocks) { return rl::debug_stamps_stream(host, nblocks); }
 int rl_debug_stamps_lat(unsigned long long* host, int nblocks) { return rl::debug_stamps_lat(host, nblocks); }
+int rl_debug_stamps_mid(unsigned long long* host, int nblocks) { return rl::debug_stamps_mid(host, nblocks); }
 #endif
 #ifdef RL_COUNT
 // diagnostic builds only: corridor work counters of the stream kernel's translation unit

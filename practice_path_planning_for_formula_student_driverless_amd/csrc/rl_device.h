@@ -57,25 +57,78 @@ struct VConst {
     double h, two_h;
 };
 
+// IEEE maxNum / minNum on the fp64 VALU (one instruction each).  They equal the
+// reference's std::max(lo, x) / std::min(hi, x) select forms for every x unless a
+// bound is a zero: v_max_f64(-0, +0) = +0 where std::max(-0, +0) = -0, and
+// v_min_f64(+0, -0) = -0 where std::min(+0, -0) = +0.  The projection uses them only
+// in waves whose bounds hold no such zero (PGD loop, `zb`).  Inline asm: the operands
+// need no canonicalisation (a NaN trial value would be a quiet NaN, and maxNum then
+// returns the bound, as the select form does).
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// The v-pass steps below sit on the velocity profile's serial dependency chain (each
+// step needs the previous one's value), so their latency, not their throughput, sets the
+// v-pass time.  RL_VSTEP_FAST (A/B knob) shortens that chain without changing a bit:
+//  * std::max(0.0, x) as v_max_f64(+0, x): equal for every x that is not a signalling NaN
+//    (x > 0: x; x = +0, -0, < 0, -inf or a quiet NaN: +0 both ways); one instruction
+//    instead of a compare and two selects;
+//  * the std::min's ahead of each max(0, .) as v_min_f64: the two forms differ only in
+//    the sign of a zero result (which the max(0, .) right after turns into +0 either way,
+//    also through the brake path's `+ (Fd+Fr)/m`: -0 + y and +0 + y differ only in a zero
+//    sign) or when the FIRST operand is a NaN (a_res = sqrt(max(0, .)) never is; a quiet
+//    NaN cap or power limit gives the other operand in both forms);
+//  * the power limit's divisions evaluated unconditionally (see vstep_fwd).
+// A signalling-NaN cap would make v_min_f64 return a quiet NaN where the select form
+// returns the other operand, so the caps are loaded canonicalised (vs_cap: a signalling
+// NaN quieted, every other value unchanged, zero signs included).
+#ifndef RL_VSTEP_FAST
+#define RL_VSTEP_FAST 1
+#endif
+#if RL_VSTEP_FAST
+__device__ __forceinline__ double vs_cap(double x) { return __builtin_canonicalize(x); }
+__device__ __forceinline__ double vs_max0(double x) { return vmax_f64(0.0, x); }
+__device__ __forceinline__ double vs_min(double a, double b) { return vmin_f64(a, b); }
+#else
+__device__ __forceinline__ double vs_cap(double x) { return x; }
+__device__ __forceinline__ double vs_max0(double x) { return smax(0.0, x); }
+__device__ __forceinline__ double vs_min(double a, double b) { return smin(a, b); }
+#endif
+
 // forward step of velocity_profile_forward_backward (ref:829-833):
 //   a_acc = ax_max_at(v,k).first ; return sqrt(max(0, v*v + 2*a_acc*h))
 __device__ __forceinline__ double vstep_fwd(const VConst& c, double vi, double ki) {
     double alat = vi * vi * fabs(ki);
-    double a_res = sqrt(smax(0.0, c.a_total2 - alat * alat));
+    double a_res = sqrt(vs_max0(c.a_total2 - alat * alat));
     double Fd = c.kFd * vi * vi;
+#if RL_VSTEP_FAST
+    // evaluated unconditionally and selected: as the arm of a branch its two divisions ran
+    // after the a_res chain instead of beside it (a discarded value has no effect)
+    const double ap = c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass;
+    double a_power = (c.Pmax > 0 && vi > 1e-6) ? ap : 1e9;
+#else
     double a_power = (c.Pmax > 0 && vi > 1e-6) ? (c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass) : 1e9;
-    double a_acc = smin(smin(a_res, c.acc_cap), a_power);
-    a_acc = smax(0.0, a_acc);
-    return sqrt(smax(0.0, __builtin_fma(2.0, a_acc * c.h, vi * vi)));   // 2*(a*h) is exact: the sum's one rounding
+#endif
+    double a_acc = vs_min(vs_min(a_res, c.acc_cap), a_power);   // std::min({a_res, cap, a_power}) ref:818
+    a_acc = vs_max0(a_acc);
+    return sqrt(vs_max0(__builtin_fma(2.0, a_acc * c.h, vi * vi)));   // 2*(a*h) is exact: the sum's one rounding
 }
 // backward step (ref:841-845): a_brk = ax_max_at(v,k).second
 __device__ __forceinline__ double vstep_bwd(const VConst& c, double vi, double ki) {
     double alat = vi * vi * fabs(ki);
-    double a_res = sqrt(smax(0.0, c.a_total2 - alat * alat));
+    double a_res = sqrt(vs_max0(c.a_total2 - alat * alat));
     double Fd = c.kFd * vi * vi;
-    double a_brk = smin(a_res, c.brk_cap) + (Fd + c.Fr) / c.mass;
-    a_brk = smax(0.0, a_brk);
-    return sqrt(smax(0.0, __builtin_fma(2.0, a_brk * c.h, vi * vi)));
+    double a_brk = vs_min(a_res, c.brk_cap) + (Fd + c.Fr) / c.mass;
+    a_brk = vs_max0(a_brk);
+    return sqrt(vs_max0(__builtin_fma(2.0, a_brk * c.h, vi * vi)));
 }
 
 }  // namespace rl

@@ -71,6 +71,8 @@ hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
 // the launches of the latency shapes lat_shape(p.N) and of every (4, 512) shape (also the
 // min-time shape for 1024 < N <= 2048 below two instances per CU), rl_kernels_lat.hip
 hipError_t launch_optimize_lat(const KParams& p, bool mintime, hipStream_t st);
+// the (4, 512) launches (1024 < N <= 2048), rl_kernels_mid.hip
+hipError_t launch_optimize_mid(const KParams& p, bool mintime, hipStream_t st);
 // large-N variant: one 1024-thread workgroup per instance, state in HBM
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st);
 // step 6 geometry (rl_geom.hip): spline knots [5][nk] per axis (s,a,b,c,d), rows [Kmax+dup][9]
@@ -102,6 +104,7 @@ int format_rows(const double* table, int64_t rows, int cols, char* out, uint64_t
 int debug_stamps(unsigned long long* host, int nblocks);
 int debug_stamps_stream(unsigned long long* host, int nblocks);
 int debug_stamps_lat(unsigned long long* host, int nblocks);
+int debug_stamps_mid(unsigned long long* host, int nblocks);
 #endif
 #ifdef RL_COUNT
 int debug_counts(unsigned long long* host, int reset);

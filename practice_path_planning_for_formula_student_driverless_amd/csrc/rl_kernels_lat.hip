@@ -10,6 +10,8 @@
 // shapes while the batch needs at most one wave per SIMD in them.  Results equal the
 // throughput shapes' bit for bit except the lap sum's tree order (the same kernel
 // template; every per-sample expression and every J / decrease sum is the same).
+// The (4, 512) shape has a translation unit of its own (rl_kernels_mid.hip) so that each
+// can be compiled with the instruction scheduler that suits it (build.py TU_FLAGS).
 #include "rl_optimize_body.h"
 
 namespace rl {
@@ -45,7 +47,7 @@ hipError_t launch_optimize_lat(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 256) return launch_lat_kt<RL_LAT1_K, 256 / RL_LAT1_K>(p, mintime, st);
     if (p.N <= 512) return launch_lat_kt<RL_LAT2_K, 512 / RL_LAT2_K>(p, mintime, st);
     if (p.N <= 1024) return launch_lat_kt<RL_LAT3_K, 1024 / RL_LAT3_K>(p, mintime, st);
-    return launch_lat_kt<4, 512>(p, mintime, st);      // = RL_MIDMT_K, RL_MIDMT_T for min-time
+    return launch_optimize_mid(p, mintime, st);       // (4, 512): rl_kernels_mid.hip
 }
 
 }  // namespace rl

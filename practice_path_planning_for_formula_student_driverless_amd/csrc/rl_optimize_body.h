@@ -139,23 +139,7 @@ __device__ __forceinline__ void wave_sum2(double& x, double& y) {
     x = readlane(x, 63);
     y = readlane(y, 63);
 }
-// IEEE maxNum / minNum on the fp64 VALU (one instruction each).  They equal the
-// reference's std::max(lo, x) / std::min(hi, x) select forms for every x unless a
-// bound is a zero: v_max_f64(-0, +0) = +0 where std::max(-0, +0) = -0, and
-// v_min_f64(+0, -0) = -0 where std::min(+0, -0) = +0.  The projection uses them only
-// in waves whose bounds hold no such zero (PGD loop, `zb`).  Inline asm: the operands
-// need no canonicalisation (a NaN trial value would be a quiet NaN, and maxNum then
-// returns the bound, as the select form does).
-__device__ __forceinline__ double vmax_f64(double a, double b) {
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ double vmin_f64(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
+// (vmax_f64 / vmin_f64: rl_device.h)
 // x + (the same register of the lane 16 (permlane16) / 32 (permlane32) rows away): the
 // swap exchanges the odd rows of one copy with the even rows of the other, so the two
 // copies afterwards hold (r0,r0,r2,r2) and (r1,r1,r3,r3) (resp. the half-waves), and their
@@ -200,6 +184,8 @@ __device__ __forceinline__ int opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+// materialise x here (the value cannot be sunk past this point into a later branch)
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
 
 // a[idx] for a runtime idx as a bit-mask blend: a select chain would be turned
 // into an indexed load, which forces the whole array out of VGPRs into scratch
@@ -453,6 +439,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #define RL_GHOST 1
 #endif
     constexpr bool GHOST = RL_GHOST && NW > 1 && K <= 2;
+    // Speculative gradient (latency shapes): every trial's gradient is evaluated before its
+    // Armijo test (the bundled tracks accept 120 of 122-137 trials per outer iteration), so
+    // the gradient's LDS reads and arithmetic run beside the J/decrease sums instead of
+    // after them.  A rejected trial's gradient is discarded; nothing else changes.
+#ifndef RL_SPEC_GRAD
+#define RL_SPEC_GRAD 1
+#endif
+    constexpr bool SPEC = RL_SPEC_GRAD && GHOST;
     constexpr int KT = K * T;
     __shared__ double gq[GHOST ? 2 * 3 * KT : 1];      // [parity][q1 | q2 | D1α][sample]
     __shared__ double gred[GHOST ? 2 * 2 * NW : 1];    // [parity][J | decrease][wave]
@@ -595,7 +589,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;     // ref:810 constant prefix
         vc.Fr = C.mass_kg * 9.81 * C.c_rr;                   // ref:811
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
-        vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
+        vc.acc_cap = vs_cap(C.a_long_acc_cap); vc.brk_cap = vs_cap(C.a_long_brake_cap);
         vc.h = h; vc.two_h = two_h;          // two_h = uni(2*h): the same value, from an SGPR pair
         sm.vc = vc;          // first read after the outer loop's first barrier
     }
@@ -1255,6 +1249,37 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             if (it >= max_inner) return 0;
             ++it;
             int bt = 0;
+            if constexpr (SPEC) {
+                for (;;) {
+                    project(cur, g, nxt);
+                    double Jn = eval_j(nxt, cur, g, true, dec);
+                    ++evals;
+                    // the trial's gradient before the Armijo test, so its LDS reads and
+                    // arithmetic overlap the J sums (pinned here: not sunk into the branch)
+                    double gt[K];
+                    const double gL0 = gL, gR0 = gR;
+                    eval_grad(gt);
+#pragma unroll
+                    for (int k = 0; k < K; ++k) pin(gt[k]);
+                    pin(gL);
+                    pin(gR);
+                    if (Jn <= J + armijo_c * dec) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k) g[k] = gt[k];
+                        cL = tL; cR = tR;
+                        J = Jn;
+                        ++accepts;
+                        break;
+                    }
+                    gL = gL0; gR = gR0;                  // a rejected trial keeps the gradient
+                    step *= 0.5;
+                    bt++;
+                    if (step < step_min || bt >= 20) return 0;
+                }
+                if (fabs(J_prev - J) < 1e-10) return 1;
+                J_prev = J;
+                return 2;
+            }
             for (;;) {
                 project(cur, g, nxt);
                 double Jn = eval_j(nxt, cur, g, true, dec);

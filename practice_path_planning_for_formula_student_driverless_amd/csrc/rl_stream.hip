@@ -284,7 +284,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;
         vc.Fr = C.mass_kg * 9.81 * C.c_rr;
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
-        vc.acc_cap = C.a_long_acc_cap; vc.brk_cap = C.a_long_brake_cap;
+        vc.acc_cap = vs_cap(C.a_long_acc_cap); vc.brk_cap = vs_cap(C.a_long_brake_cap);
         vc.h = h; vc.two_h = two_h;      // two_h = uni(2*h): the same value, from an SGPR pair
         sm.vc = vc;                      // first read after the outer loop's first barrier
     }

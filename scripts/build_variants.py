@@ -39,7 +39,20 @@ VARIANTS = {
     "lat2k1": {"RL_LAT2_K": 1},          # (1,512) for 256 < N <= 512 (8 waves, one sample per lane)
     "probe_nob1": {"RL_PROBE_NOB1": 1},
     "ghost0": {"RL_GHOST": 0},
-    "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)           # latency shapes with the two-barrier evaluation (A/B of the ghost samples)  # timing probe (wrong results): scripts/probe_lat.py
+    "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)
+    "spec0": {"RL_SPEC_GRAD": 0},        # latency shapes without the speculative gradient
+    "vfast0": {"RL_VSTEP_FAST": 0},      # v-pass steps with the select forms of max(0, .) / min
+    # scheduler A/B (build.py TU_FLAGS holds the product's choice; "_tu" overrides per source)
+    "lat_default": {"_tu": {"csrc/rl_kernels_lat.hip": []}},
+    "mid_default": {"_tu": {"csrc/rl_kernels_mid.hip": []}},
+    "mid_ilp": {"_tu": {"csrc/rl_kernels_mid.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}},
+    "lat_iilp": {"_tu": {"csrc/rl_kernels_lat.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}},
+    "thr_ilp": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}},
+    "thr_minreg": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]}},
+    "thr_memclause": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}},
+    "thr_maxocc": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]}},
+    # (iterative-ilp on rl_kernels.hip crashes this LLVM's register allocator on <8,256,closed,mintime>)
+    "stream_iilp": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
 }

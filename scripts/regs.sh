@@ -2,7 +2,7 @@
 # Per-kernel VGPR / scratch / occupancy report of the gfx950 kernels (static, no GPU).
 # One line per kernel: <K,T,closed,mintime,ragged> (or the streaming kernel's <closed,mintime>).
 cd "$(dirname "$0")/../practice_path_planning_for_formula_student_driverless_amd/csrc" || exit 1
-for f in rl_kernels.hip rl_kernels_lat.hip rl_stream.hip; do
+for f in rl_kernels.hip rl_kernels_lat.hip rl_kernels_mid.hip rl_stream.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -I../../include \
     --cuda-device-only -c "$f" -o /tmp/_regs.o -Rpass-analysis=kernel-resource-usage "$@" 2>&1 |
     grep -E "Function Name|VGPRs:|ScratchSize|Occupancy" | sed -E 's/.*remark: //; s/ \[-Rpass-analysis=kernel-resource-usage\]//' |

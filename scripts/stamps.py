@@ -17,10 +17,11 @@ for cname, B, modes in (("cmap1_n2000", 1024, 1), ("cmap1_n2000_vp20", 256, 2), 
     assert lib.rl_plan_run(h, None) == 0
     ms = C.c_float(); lib.rl_plan_kernel_ms(h, modes, C.byref(ms))
     st = np.zeros((B, 16), dtype=np.uint64)
-    # the latency shapes and every (4, 512) live in rl_kernels_lat.hip, which has its own stamps
+    # the latency shapes live in rl_kernels_lat.hip and every (4, 512) in rl_kernels_mid.hip,
+    # each with its own stamps
     K, T = abi.kernel_shape(prob.N, B, modes)
-    lat = (K, T) == (4, 512) or K <= 2
-    assert (lib.rl_debug_stamps_lat if lat else lib.rl_debug_stamps)(st.ctypes.data_as(C.c_void_p), B) == 0
+    f = lib.rl_debug_stamps_mid if (K, T) == (4, 512) else lib.rl_debug_stamps_lat if K <= 2 else lib.rl_debug_stamps
+    assert f(st.ctypes.data_as(C.c_void_p), B) == 0
     tot = st.sum(0).astype(float)
     print(f"{cname} B={B} mode={modes} shape=({K},{T}) kernel {ms.value:.2f} ms; per-block cycles {tot.sum()/B:.3e}")
     for i, nm in enumerate(names):

@@ -1,6 +1,6 @@
 """Phase shares of one-instance (drop-in) runs from the RL_STAMPS diagnostic build: the
 latency shape (rl_kernels_lat.hip's stamps) against the throughput shape (RL_LAT_SHAPES=0,
-rl_kernels.hip's stamps; (4, 512) lives in the latency unit).  Shares only: a stamped
+rl_kernels.hip's stamps; (4, 512) lives in rl_kernels_mid.hip).  Shares only: a stamped
 build's absolute time is not the real kernel's."""
 import ctypes as C, os, sys, numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,8 +22,8 @@ for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n20
             assert lib.rl_plan_run(h, None) == 0
             ms = C.c_float(); lib.rl_plan_kernel_ms(h, mode, C.byref(ms))
             st = np.zeros((1, 16), dtype=np.uint64)
-            in_lat = (not thr) or (K, T) == (4, 512)
-            f = lib.rl_debug_stamps_lat if in_lat else lib.rl_debug_stamps
+            f = (lib.rl_debug_stamps_mid if (K, T) == (4, 512) else
+                 lib.rl_debug_stamps_lat if not thr else lib.rl_debug_stamps)
             assert f(st.ctypes.data_as(C.c_void_p), 1) == 0
             tot = st.sum(0).astype(float)
             print(f"{cname} N={prob.N} mode={mode} shape=({K},{T}) kernel {ms.value:.3f} ms (stamped); "
