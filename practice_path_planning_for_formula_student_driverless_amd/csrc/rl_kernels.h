@@ -55,7 +55,13 @@ struct Shape {
 #ifndef RL_LAT3_K
 #define RL_LAT3_K 2      // N <= 1024: (2, 512)
 #endif
+// RL_LAT_FIT: for N <= 512 one sample per lane on just enough waves, T = max(128, N rounded
+// up to 64) (fewer waves: a cheaper barrier and cross-wave sum per evaluation)
+#ifndef RL_LAT_FIT
+#define RL_LAT_FIT 0
+#endif
 inline Shape lat_shape(int N) {
+    if (RL_LAT_FIT && N <= 512) return {1, N <= 128 ? 128 : (N + 63) / 64 * 64};
     if (N <= 256) return {RL_LAT1_K, 256 / RL_LAT1_K};
     if (N <= 512) return {RL_LAT2_K, 512 / RL_LAT2_K};
     if (N <= 1024) return {RL_LAT3_K, 1024 / RL_LAT3_K};

@@ -29,7 +29,7 @@ static hipError_t launch_lat_t(const KParams& p, hipStream_t st) {
 }
 template <int K, int T>
 static hipError_t launch_lat_kt(const KParams& p, bool mt, hipStream_t st) {
-    static_assert(K * T == 256 || K * T == 512 || K * T == 1024 || K * T == 2048, "latency shape");
+    static_assert(T % 64 == 0 && T <= 512, "latency shape");
     if (p.closed) return mt ? launch_lat_t<K, T, true, true>(p, st) : launch_lat_t<K, T, true, false>(p, st);
     return mt ? launch_lat_t<K, T, false, true>(p, st) : launch_lat_t<K, T, false, false>(p, st);
 }
@@ -44,6 +44,19 @@ int debug_stamps_lat(unsigned long long* host, int nblocks) {
 
 hipError_t launch_optimize_lat(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || p.N > 2048) return hipErrorInvalidValue;
+#if RL_LAT_FIT
+    if (p.N <= 512) {
+        switch (lat_shape(p.N).T) {
+            case 128: return launch_lat_kt<1, 128>(p, mintime, st);
+            case 192: return launch_lat_kt<1, 192>(p, mintime, st);
+            case 256: return launch_lat_kt<1, 256>(p, mintime, st);
+            case 320: return launch_lat_kt<1, 320>(p, mintime, st);
+            case 384: return launch_lat_kt<1, 384>(p, mintime, st);
+            case 448: return launch_lat_kt<1, 448>(p, mintime, st);
+            default: return launch_lat_kt<1, 512>(p, mintime, st);
+        }
+    }
+#endif
     if (p.N <= 256) return launch_lat_kt<RL_LAT1_K, 256 / RL_LAT1_K>(p, mintime, st);
     if (p.N <= 512) return launch_lat_kt<RL_LAT2_K, 512 / RL_LAT2_K>(p, mintime, st);
     if (p.N <= 1024) return launch_lat_kt<RL_LAT3_K, 1024 / RL_LAT3_K>(p, mintime, st);

@@ -15,7 +15,7 @@ for p in sorted(glob.glob(os.path.join(REPO, "practice_path_planning_for_formula
     if not (n in ("stamps", "count") or n.startswith("probe")):
         libs[n] = abi.load_library(p)
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
-CASES = ["track_training_map", "track_competition_map_testday3", "cmap1_n2000"]
+CASES = ["track_training_map", "track_competition_map1", "track_competition_map_testday3", "cmap1_n2000"]
 res = {}
 for cname in CASES:
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)

@@ -42,6 +42,7 @@ VARIANTS = {
     "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)
     "spec0": {"RL_SPEC_GRAD": 0},        # latency shapes without the speculative gradient
     "vfast0": {"RL_VSTEP_FAST": 0},      # v-pass steps with the select forms of max(0, .) / min
+    "latfit": {"RL_LAT_FIT": 1},         # K = 1 latency shapes on just enough waves for N <= 512
     # scheduler A/B (build.py TU_FLAGS holds the product's choice; "_tu" overrides per source)
     "lat_default": {"_tu": {"csrc/rl_kernels_lat.hip": []}},
     "mid_default": {"_tu": {"csrc/rl_kernels_mid.hip": []}},
