@@ -56,9 +56,11 @@ struct Shape {
 #define RL_LAT3_K 2      // N <= 1024: (2, 512)
 #endif
 // RL_LAT_FIT: for N <= 512 one sample per lane on just enough waves, T = max(128, N rounded
-// up to 64) (fewer waves: a cheaper barrier and cross-wave sum per evaluation)
+// up to 64): fewer waves make the evaluation's barrier and cross-wave sum cheaper (A/B:
+// testday3 N=261 (1, 512) -> (1, 320) 1.76 -> 1.68 ms min-curv, 2.25 -> 2.16 ms min-time;
+// 0 keeps the RL_LAT1_K / RL_LAT2_K table)
 #ifndef RL_LAT_FIT
-#define RL_LAT_FIT 0
+#define RL_LAT_FIT 1
 #endif
 inline Shape lat_shape(int N) {
     if (RL_LAT_FIT && N <= 512) return {1, N <= 128 ? 128 : (N + 63) / 64 * 64};

@@ -42,7 +42,7 @@ VARIANTS = {
     "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)
     "spec0": {"RL_SPEC_GRAD": 0},        # latency shapes without the speculative gradient
     "vfast0": {"RL_VSTEP_FAST": 0},      # v-pass steps with the select forms of max(0, .) / min
-    "latfit": {"RL_LAT_FIT": 1},         # K = 1 latency shapes on just enough waves for N <= 512
+    "latfit0": {"RL_LAT_FIT": 0},        # the (1, 256) / (1, 512) latency table instead of K = 1 on just enough waves
     # scheduler A/B (build.py TU_FLAGS holds the product's choice; "_tu" overrides per source)
     "lat_default": {"_tu": {"csrc/rl_kernels_lat.hip": []}},
     "mid_default": {"_tu": {"csrc/rl_kernels_mid.hip": []}},
@@ -51,7 +51,8 @@ VARIANTS = {
     "thr_ilp": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}},
     "thr_minreg": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]}},
     "thr_memclause": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}},
-    "thr_maxocc": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]}},
+    "thr_default": {"_tu": {"csrc/rl_kernels.hip": []}},
+    "stream_maxocc": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]}},
     # (iterative-ilp on rl_kernels.hip crashes this LLVM's register allocator on <8,256,closed,mintime>)
     "stream_iilp": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed

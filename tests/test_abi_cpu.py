@@ -122,13 +122,19 @@ def test_kernel_shape_table():
     """Throughput shapes for batches that fill the GPU, latency shapes (one instance over a
     CU) while the batch needs at most one wave per SIMD in them (256 CUs assumed here)."""
     MC, MT = abi.RL_MODE_MINCURV, abi.RL_MODE_MINTIME
+    # K = 1 on just enough waves up to N = 512 (RL_LAT_FIT)
+    assert abi.kernel_shape(1, 1, MC) == (1, 128)
+    assert abi.kernel_shape(128, 1, MC) == (1, 128)
+    assert abi.kernel_shape(187, 1, MT) == (1, 192)
     assert abi.kernel_shape(216, 1, MC) == (1, 256)
     assert abi.kernel_shape(216, 256, MC) == (1, 256)
     assert abi.kernel_shape(216, 257, MC) == (4, 64)
-    assert abi.kernel_shape(261, 1, MT) == (1, 512)
-    assert abi.kernel_shape(261, 128, MC) == (1, 512)
-    assert abi.kernel_shape(261, 129, MC) == (8, 64)
+    assert abi.kernel_shape(261, 1, MT) == (1, 320)
+    assert abi.kernel_shape(261, 204, MC) == (1, 320)
+    assert abi.kernel_shape(261, 205, MC) == (8, 64)
     assert abi.kernel_shape(261, 512, MT) == (8, 64)
+    assert abi.kernel_shape(392, 1, MC) == (1, 448)
+    assert abi.kernel_shape(512, 1, MT) == (1, 512)
     assert abi.kernel_shape(2000, 1, MC) == (4, 512)
     assert abi.kernel_shape(2000, 1, MT) == (4, 512)
     assert abi.kernel_shape(1000, 8, MC) == (2, 512)

@@ -211,12 +211,12 @@ def _synthetic(N, closed, rng):
 
 @pytest.mark.parametrize("shapes", SHAPES)
 @pytest.mark.parametrize("closed", [True, False])
-@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 8, 63, 64, 65, 255, 256, 257, 392, 512, 1000, 1023, 1025, 1536, 2047,
-                               2048, 2049, 3072, 4096])
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 8, 63, 64, 65, 150, 255, 256, 257, 330, 380, 392, 512, 1000, 1023, 1025,
+                               1536, 2047, 2048, 2049, 3072, 4096])
 def test_ragged_sizes_vs_oracle(N, closed, shapes, monkeypatch):
     """Every kernel variant (K,T) and every partial-chunk shape, closed and open, in the
-    latency shapes (B = 2: (1, 256), (2, 256), (2, 512), (4, 512); general per-sample
-    stencils for open tracks, K <= 2) and the throughput shapes.  Open multiples of K >= 4
+    latency shapes (B = 2: (1, T) for T = 128 ... 512 in steps of 64, (2, 512), (4, 512);
+    general per-sample stencils for open tracks, K <= 2) and the throughput shapes.  Open multiples of K >= 4
     take the interior stencils with the boundary selects (rl_optimize_body.h OPEN_FAST):
     one lane holding both ends (4, 8), a single wave with its last active lane inside (392)
     or at lane 63 (512), and three or more waves per instance (1536, 2048, 3072, 4096),
