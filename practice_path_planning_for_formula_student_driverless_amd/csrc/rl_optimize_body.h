@@ -84,6 +84,15 @@ static __device__ unsigned long long rl_dbg_stamps[16384][16];   // per translat
 #else
 #define RL_STAMP(slot) do {} while (0)
 #endif
+// finer stamps inside the latency shapes' evaluation (-DRL_STAMPS_EVAL=1 with RL_STAMPS):
+// 11 projection, 12 stencil + partial sums + LDS writes, 13 wave sum, 14 barrier + block
+// sum + Armijo test, 15 gradient.  Each stamp serialises the code around it, so the shares
+// are indicative only.
+#if defined(RL_STAMPS) && defined(RL_STAMPS_EVAL)
+#define RL_ESTAMP(slot) RL_STAMP(slot)
+#else
+#define RL_ESTAMP(slot) do {} while (0)
+#endif
 
 // std::pow for a non-default time_gamma_power (ref:960), out of line: inlined, its
 // temporaries competed with the kernel's live state for registers (min-time (8,256):
@@ -438,7 +447,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #ifndef RL_GHOST
 #define RL_GHOST 1
 #endif
-    constexpr bool GHOST = RL_GHOST && NW > 1 && K <= 2;
+#ifndef RL_GHOST_KMAX
+#define RL_GHOST_KMAX 2      // ghost samples for K <= this (A/B knob)
+#endif
+    constexpr bool GHOST = RL_GHOST && NW > 1 && K <= RL_GHOST_KMAX;
     // Speculative gradient (latency shapes): every trial's gradient is evaluated before its
     // Armijo test (the bundled tracks accept 120 of 122-137 trials per outer iteration), so
     // the gradient's LDS reads and arithmetic run beside the J/decrease sums instead of
@@ -851,33 +863,23 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // of the trial vector a: J (uniform across the workgroup) and the Armijo
     // decrease Σ grad*(a-α) (ref:733 / 1009); q1,q2,D1α and their in-wave
     // neighbours are left for eval_grad.
-    auto eval_j = [&](double (&a)[K], const double (&cur)[K], const double (&g)[K], bool trial,
-                      double& dec) RL_AI -> double {
-        // J and the Armijo decrease only steer accept/stop decisions; the α iterates
-        // never read them, so their accumulations use fma (their summation order
-        // already differs from the reference's serial loop, ref:661-666)
+    // Σ g·(a − cur) over this lane's samples (the Armijo decrease, ref:733 / 1009)
+    auto part_dec = [&](const double (&a)[K], const double (&cur)[K], const double (&g)[K]) RL_AI -> double {
         double pdec = 0.0;
-        if (trial) {
-            if (part_wave) {
+        if (part_wave) {
 #pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (k < cnt) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
-            } else {
-#pragma unroll
-                for (int k = 0; k < K; ++k) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
-            }
-        }
-        double lv, rv;
-        if constexpr (GHOST) {               // the neighbours' values of a: no exchange
-            lv = trial ? tL : cL;
-            rv = trial ? tR : cR;
+            for (int k = 0; k < K; ++k)
+                if (k < cnt) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
         } else {
-            xpub(0, a);
-#ifndef RL_PROBE_NOB1       // timing probe only (wrong results): the trial halo's barrier removed
-            if constexpr (NW > 1) __syncthreads();
-#endif
-            xget(0, a, lv, rv);
+#pragma unroll
+            for (int k = 0; k < K; ++k) pdec = __builtin_fma(g[k], a[k] - cur[k], pdec);
         }
+        return pdec;
+    };
+    // the lane's part of one evaluation of a, given its neighbours' values lv, rv: the
+    // residuals, this lane's J terms (returned) and the stencil inputs q1, q2, D1α, published
+    // for the gradient (GHOST: LDS buffer gpar; else the halo exchange slots)
+    auto eval_part = [&](double (&a)[K], double lv, double rv) RL_AI -> double {
         fill_pad(a, rv);
         double pJ = 0.0, pJsm = 0.0;
         double jr[K];
@@ -925,16 +927,40 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
         pJ = __builtin_fma(lam_act, pJsm, pJ);         // J += λ·Jsm (ref:663 / 883), per lane
         if constexpr (GHOST) {
+            // every lane writes its K slots (base + k < K*T): a padding sample's slot is never
+            // read, and unmasked stores keep the evaluation one basic block
             double* const Q = &gq[gpar * 3 * KT];
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (k < cnt) { Q[base + k] = q1[k]; Q[KT + base + k] = q2[k]; Q[2 * KT + base + k] = a1v[k]; }
+            for (int k = 0; k < K; ++k) { Q[base + k] = q1[k]; Q[KT + base + k] = q2[k]; Q[2 * KT + base + k] = a1v[k]; }
         } else {
             xpub(1, q1);
             xpub(2, q2);
             xpub(3, a1v);
         }
+        return pJ;
+    };
+    auto eval_j = [&](double (&a)[K], const double (&cur)[K], const double (&g)[K], bool trial,
+                      double& dec) RL_AI -> double {
+        // J and the Armijo decrease only steer accept/stop decisions; the α iterates
+        // never read them, so their accumulations use fma (their summation order
+        // already differs from the reference's serial loop, ref:661-666)
+        const double pdec = trial ? part_dec(a, cur, g) : 0.0;
+        double lv, rv;
+        RL_ESTAMP(11);
+        if constexpr (GHOST) {               // the neighbours' values of a: no exchange
+            lv = trial ? tL : cL;
+            rv = trial ? tR : cR;
+        } else {
+            xpub(0, a);
+#ifndef RL_PROBE_NOB1       // timing probe only (wrong results): the trial halo's barrier removed
+            if constexpr (NW > 1) __syncthreads();
+#endif
+            xget(0, a, lv, rv);
+        }
+        const double pJ = eval_part(a, lv, rv);
+        RL_ESTAMP(12);
         const double z = wave_sum_xy(pJ, pdec, lane & 1);   // lane 0: Σ J terms, lane 1: Σ decrease
+        RL_ESTAMP(13);
         if constexpr (NW == 1) {             // the wave sums are the block sums
             dec = readlane(z, 1);
             return readlane(z, 0);
@@ -949,6 +975,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             dec = D;
             gpar_last = gpar;
             gpar ^= 1;
+            RL_ESTAMP(14);
             return J;
         }
         if (lane < 2) sm.red[lane][wid] = z;
@@ -1263,6 +1290,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     for (int k = 0; k < K; ++k) pin(gt[k]);
                     pin(gL);
                     pin(gR);
+                    RL_ESTAMP(15);
                     if (Jn <= J + armijo_c * dec) {
 #pragma unroll
                         for (int k = 0; k < K; ++k) g[k] = gt[k];

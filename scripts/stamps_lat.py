@@ -7,9 +7,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "tests"))
 import oracle_lib as O
 from practice_path_planning_for_formula_student_driverless_amd import abi
-lib = abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_stamps.so"))
-names = ["setup", "corridor tail", "mt:κ/vpass/γ", "lin-geom", "PGD loop", "update", "final",
-         "normals + corridor loads", "corridor: inner rays", "corridor: outer rays", "corridor: fallback"]
+# usage: python scripts/stamps_lat.py [variant]   (stamps, or stamps_eval for the evaluation's phases)
+VAR = sys.argv[1] if len(sys.argv) > 1 else "stamps"
+lib = abi.load_library(os.path.join(REPO, f"practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_{VAR}.so"))
+names = ["setup", "corridor tail", "mt:κ/vpass/γ", "lin-geom", "PGD loop (rest)", "update", "final",
+         "normals + corridor loads", "corridor: inner rays", "corridor: outer rays", "corridor: fallback",
+         "pgd: projection", "pgd: stencil+partials", "pgd: wave sum", "pgd: barrier+block sum", "pgd: gradient"]
 for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n2000"):
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)
     for mode in (1, 2):
