@@ -136,7 +136,16 @@ __device__ unsigned long long rl_dbg_stamps_s[16384][16];
 #endif
 
 template <bool CLOSED, bool MT>
+// RL_STS_MINW: minimum waves per SIMD the register budget must allow (0: the compiler's
+// choice for TS), e.g. TS = 512 with 4 keeps two instances co-resident per CU (A/B knob)
+#ifndef RL_STS_MINW
+#define RL_STS_MINW 0
+#endif
+#if RL_STS_MINW
+__global__ __launch_bounds__(TS, RL_STS_MINW) void rl_stream_kernel(KParams p, StreamBufs sb) {
+#else
 __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb) {
+#endif
     __shared__ SSmem sm;
 #ifdef RL_STAMPS
     unsigned long long st_acc[16] = {};

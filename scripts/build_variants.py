@@ -42,7 +42,9 @@ VARIANTS = {
     "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)
     "spec0": {"RL_SPEC_GRAD": 0},        # latency shapes without the speculative gradient
     "vfast0": {"RL_VSTEP_FAST": 0},      # v-pass steps with the select forms of max(0, .) / min
-    "latfit0": {"RL_LAT_FIT": 0},        # the (1, 256) / (1, 512) latency table instead of K = 1 on just enough waves
+    "latfit0": {"RL_LAT_FIT": 0},
+    "sts512": {"RL_STS": 512, "RL_STS_MINW": 4},   # streaming kernel: two 512-thread instances per CU
+    "sts256": {"RL_STS": 256, "RL_STS_MINW": 4},   # four 256-thread instances per CU        # the (1, 256) / (1, 512) latency table instead of K = 1 on just enough waves
     # scheduler A/B (build.py TU_FLAGS holds the product's choice; "_tu" overrides per source)
     "lat_default": {"_tu": {"csrc/rl_kernels_lat.hip": []}},
     "mid_default": {"_tu": {"csrc/rl_kernels_mid.hip": []}},
