@@ -1243,7 +1243,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         for (int k = 0; k < K; ++k)
             zb_lane |= (__double_as_longlong(lo[k]) == (long long)0x8000000000000000ull) ||
                        (hi[k] == 0.0 && k < cnt);
+#ifdef RL_PROBE_NOZB      // timing probe only (zero signs may differ): every clamp as maxNum/minNum
+        const bool zb = false;
+        (void)zb_lane;
+#else
         const bool zb = __builtin_amdgcn_ballot_w64(zb_lane) != 0;
+#endif
         double step = step_init;
         // trial vector std::min(hi, std::max(lo, cur - step*grad)) (ref:731)
         auto project = [&](const double (&cur)[K], const double (&g)[K], double (&nxt)[K]) RL_AI {
@@ -1258,8 +1263,13 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 for (int k = 0; k < K; ++k) nxt[k] = smin(hi[k], smax(lo[k], ai[k]));   // the select forms
             }
             if constexpr (GHOST) {               // the neighbour samples' trial values
+#ifdef RL_PROBE_NOZB
+                tL = vmin_f64(hiL, vmax_f64(loL, cL - step * gL));
+                tR = vmin_f64(hiR, vmax_f64(loR, cR - step * gR));
+#else
                 tL = smin(hiL, smax(loL, cL - step * gL));
                 tR = smin(hiR, smax(loR, cR - step * gR));
+#endif
             }
         };
         double dec;

@@ -38,6 +38,8 @@ VARIANTS = {
     "lat1k2": {"RL_LAT1_K": 2},          # (2,128) for N <= 256 (ghost samples at K = 2)
     "lat2k1": {"RL_LAT2_K": 1},          # (1,512) for 256 < N <= 512 (8 waves, one sample per lane)
     "probe_nob1": {"RL_PROBE_NOB1": 1},
+    "probe_nozb": {"RL_PROBE_NOZB": 1},
+    "zbghost0": {"RL_ZB_GHOST": 0},      # the ghost samples' clamps always in the select forms  # timing probe: every projection clamp as maxNum/minNum (zero signs may differ)
     "ghost0": {"RL_GHOST": 0},
     "along": {"RL_ALONG": 1},            # along-ray corridor block culling (rl_corridor.h)
     "spec0": {"RL_SPEC_GRAD": 0},        # latency shapes without the speculative gradient

@@ -1,14 +1,16 @@
-"""Timing probe: time per evaluation of one-instance runs (latency shapes) with and without
-the trial halo's barrier (variant probe_nob1 gives wrong results; only its time per
-evaluation, kernel ms / evaluations, is read).  Plan path, B=1, min-curv."""
+"""Timing probe: time per evaluation of one-instance runs (latency shapes) of the product
+against timing-probe variants (probe_nob1: no trial-halo barrier; probe_nozb: every clamp as
+maxNum/minNum; their results may be wrong, only the time per evaluation, kernel ms /
+evaluations, is read).  Plan path, min-curv.  usage: probe_lat.py [variant ...]"""
 import ctypes as C, os, sys, json
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "tests"))
 import oracle_lib as O
 from practice_path_planning_for_formula_student_driverless_amd import abi
-libs = {"base": abi.load_library(),
-        "nob1": abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_probe_nob1.so"))}
+libs = {"base": abi.load_library()}
+for v in (sys.argv[1:] or ["probe_nob1"]):
+    libs[v] = abi.load_library(os.path.join(REPO, f"practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_{v}.so"))
 for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n2000"):
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)
     for B in (1, 1024):
