@@ -56,6 +56,10 @@ VARIANTS = {
     "thr_minreg": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]}},
     "thr_memclause": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}},
     "thr_default": {"_tu": {"csrc/rl_kernels.hip": []}},
+    "thr_bias0": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", "-mllvm", "-amdgpu-schedule-metric-bias=0"]}},
+    "thr_trackers": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", "-mllvm", "-amdgpu-use-amdgpu-trackers"]}},
+    "thr_def_bias0": {"_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-schedule-metric-bias=0"]}},
+    "stream_bias0": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-schedule-metric-bias=0"]}},
     "stream_maxocc": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]}},
     # (iterative-ilp on rl_kernels.hip crashes this LLVM's register allocator on <8,256,closed,mintime>)
     "stream_iilp": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}},
