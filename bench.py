@@ -141,6 +141,34 @@ def _lap_worker(job):
     return out
 
 
+ALLCORE_CORES = 16      # the host CPU share of one GPU on the box (its operator's worker-pool size)
+
+
+def reference_multicore(prob, cfg, cores, work: str, MO: int, budget_s: float = 6.0) -> dict:
+    """The reference's compute_min_curvature_raceline on C2's problem, one independent
+    instance stream per core (the instance-parallel CPU form of the batch), `len(cores)`
+    processes pinned one per core, run together for ~budget_s.  Context, not the target."""
+    import oracle_lib as O
+
+    path = os.path.join(work, "problem_mc.bin")
+    O.write_problem_bin(prob, cfg, path)
+    procs = []
+    for c in cores:
+        procs.append(subprocess.Popen([O.REF_BENCH, path, "mincurv", str(budget_s), "2"], stdout=subprocess.PIPE,
+                                      text=True, preexec_fn=(lambda c=c: os.sched_setaffinity(0, {c}))))
+    rates, calls = [], 0
+    for p in procs:
+        out, _ = p.communicate(timeout=600)
+        r = json.loads(out.strip().splitlines()[-1])
+        calls += int(r["calls"])
+        rates.append(int(r["calls"]) * MO / float(r["seconds"]))
+    return {"value": round(sum(rates), 1), "unit": "PGD outer-iters/s", "cores": len(cores), "kind": "reference",
+            "per_core_min": round(min(rates), 1), "per_core_max": round(max(rates), 1), "calls": calls,
+            "note": f"context only: {len(cores)} concurrent ref_bench_o3 processes, one pinned per core (this GPU's "
+                    f"host CPU share on the box), each ~{budget_s:.0f} s of C2 calls; the reference itself is "
+                    f"single-threaded"}
+
+
 def cpu_leg(budget_s: float) -> dict:
     """Everything the bench needs from the CPU, computed without touching the GPU:
     the baseline on one pinned core, the reference's per-track drop-in times, and the
@@ -198,6 +226,10 @@ def cpu_leg(budget_s: float) -> dict:
             ts = [float(np.median(O.run_ref_bench(p, c, mt, 0.0, 3, work)["ms"])) for mt in (False, True)]
             per[name] = {"N": p.N, "mincurv_ms": round(ts[0], 2), "mintime_ms": round(ts[1], 2)}
         res["reference_per_track"] = per
+    # ---- context only (SURVEY §8d optional): the reference instance-parallel on
+    # this GPU's host CPU share -- one ref_bench process per core, each pinned, on C2's problem
+    if have_ref and len(cores) > 3:
+        res["reference_multicore"] = reference_multicore(prob, cfg, cores[2:2 + ALLCORE_CORES], work, MO)
     # ---- oracle laps for the lap-Δ statistics (C3 sample, the whole C4 grid)
     c3case, _, cfg3 = load_problem("cmap1_n2000_vp20")
     c3_seeds = list(range(0, C3_BATCH, C3_BATCH // C3_SAMPLE))
@@ -408,8 +440,11 @@ def run_c5(world, rank, local, dev, dist):
             "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
             "achieved": round(pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9, 1) if pmc else None,
             "frac": round(pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pmc else None,
-            "basis": "measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes, "
+            "basis": "measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE x1, separate --pmc passes, "
                      "profiles/pmc_traffic.json at these kernel sources) / kernel time",
+            "counter_calibration": "x2 / x1 measured at this kernel's own 8-B/lane streaming width on a 2 GiB array "
+                                   "(scripts/fetch_calib.hip; profiles/r05/fetch_calib.json: read8 2.000, read16 "
+                                   "2.000, write8 1.000)",
             "pmc_profile": pmc.get("profile") if pmc else None,
             "model_GBps_aside": round(model / (k_ms * 1e-3) / 1e9, 1),
             "model_note": "SURVEY §8d one-pass-per-evaluation streaming bytes; batched backtracking reads the state "
@@ -587,6 +622,49 @@ def run_format(world, rank, mc_x, mc_y, mc_k, mc_al, case, cfg):
             "bytes_equal_on_sample": text[: len(cpu_text)] == cpu_text, "sample_rows": k}
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_plan(gpus: int, env, argv) -> list | None:
+    """How `bench.py --gpus N` runs (decided before anything touches the GPU).
+
+    * WORLD_SIZE unset, N == 1: this process is the single rank (None).
+    * WORLD_SIZE unset, N > 1: this process only launches N fresh ranks, one per GPU, with
+      torch.distributed.run on 127.0.0.1 (the command is returned; the parent relays rank
+      0's JSON line and the exit code).
+    * WORLD_SIZE set (launched by torch.distributed.run): it must equal N, else SystemExit.
+    """
+    if gpus < 1:
+        raise SystemExit(f"bench: --gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench: WORLD_SIZE={ws} but --gpus {gpus}: launch one rank per GPU "
+                             f"(--nproc-per-node {gpus}) or pass --gpus {ws}")
+        return None
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def backend_label(world: int, backend: str, same_device: bool) -> str:
+    """The `parallelism` string: what actually ran (backend and device placement)."""
+    if world == 1:
+        return "dp1: one GPU, no collective"
+    coll = "RCCL (torch.distributed nccl) over xGMI" if backend == "nccl" else f"torch.distributed {backend}"
+    where = (f"{world} ranks on one GPU (same-device rehearsal)" if same_device
+             else f"instances sharded over {world} GPUs, one rank per GPU")
+    return f"dp{world}: {where}; per-step {coll} gather of per-instance summaries to rank 0"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -601,6 +679,12 @@ def main():
     if args.cpu_leg:
         print(json.dumps(cpu_leg(args.cpu_budget)), flush=True)
         return
+    cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if cmd is not None:
+        # N ranks as child processes (this parent has not touched the GPU and never does);
+        # rank 0's JSON line reaches stdout through the inherited descriptor
+        rc = subprocess.run(cmd, env={**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}).returncode
+        sys.exit(rc)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -612,10 +696,14 @@ def main():
     if rank != 0 and len(HOST_CORES) > 2:
         os.sched_setaffinity(0, set(HOST_CORES) - {min(HOST_CORES)})
     # rehearsal on a one-GPU box only: every rank on cuda:0, gloo instead of RCCL
-    if os.environ.get("RL_BENCH_SAME_DEVICE") == "1":
+    same_device = os.environ.get("RL_BENCH_SAME_DEVICE") == "1"
+    if same_device:
         local = 0
     backend = os.environ.get("RL_BENCH_BACKEND", "nccl")
     import torch
+
+    if world > 1 and not same_device and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
 
     dist = None
     if world > 1:
@@ -750,6 +838,16 @@ def main():
         "frac_of_nonfma_ceiling": round(achieved_tf / FP64_NONFMA_TFLOPS, 4),
         "evals_per_outer": round(E_k, 2),
     }
+    # SURVEY §8d's streaming byte model beside the flop roofline (its achieved/8 TB/s exceeds
+    # 1 at C2: the per-evaluation state lives in VGPRs/LDS and never reaches HBM)
+    model_b = B * MO * bytes_per_outer(N, E_k, Eseg)
+    model_gbs = model_b / (k_ms * 1e-3) / 1e9
+    roofline["byte_model"] = {
+        "bytes_per_launch": model_b, "achieved_GBps": round(model_gbs, 1), "peak_GBps": HBM_PEAK_GBS,
+        "frac": round(model_gbs / HBM_PEAK_GBS, 3),
+        "model": f"SURVEY §8d: N*(80*E_k + 224) + 32*(Ei+Eo) bytes per outer, x {B}x{MO} outers",
+        "note": "frac > 1: on-chip residency -- the state stays in VGPRs/LDS across evaluations, so the HBM "
+                "roofline does not bind; the measured HBM traffic is `traffic`"}
     if pmc:
         ex = pmc.get("fp64_flops_per_launch")
         if ex:
@@ -769,6 +867,7 @@ def main():
         cpu["cpu_model"] = cpu_res["cpu"]["model"]
         cpu["host_nproc"] = cpu_res["cpu"]["nproc"]
         cpu["port_restatement"] = cpu_res["port"] if cpu_res.get("reference") else None
+        cpu["reference_multicore_context"] = cpu_res.get("reference_multicore")
         if "c3_mintime_plus_mincurv" in extras:
             c3o = cpu_res["c3_oracle_laps"]
             extras["c3_mintime_plus_mincurv"]["lap_delta_vs_oracle"] = {
@@ -809,8 +908,8 @@ def main():
         "data": "competition_map1 cones from the reference repo -> reference steps 1-6 (fixture); synthetic alpha-seeds",
         "config": {"workload": "C2: competition_map1 closed, N=2000, B=1024 alpha-seeds per GPU, min-curvature, "
                                "14 outer iterations, default cfg::Config", "N": N, "batch_per_gpu": B,
-                   "global_batch": world * B, "parallelism": f"dp{world}: instances sharded over {world} GPU(s); per-step RCCL gather of "
-                                  f"per-instance summaries to rank 0"},
+                   "global_batch": world * B, "parallelism": backend_label(world, backend, same_device),
+                   "backend": backend if world > 1 else None},
         "tracks_per_s": round(tracks_per_s, 2),
         "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         "roofline": roofline,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 4
+#define RL_ABI_VERSION 5
 
 /* error codes */
 #define RL_OK          0
@@ -184,9 +184,12 @@ int rl_plan_cache_info(int32_t* entries, int64_t* device_bytes, int64_t* pinned_
  * one plan and HIP stream per device, all devices enqueued before the first download;
  * each block's results are copied to its offset of the caller's host outputs (the final
  * gather).  devices: n_dev device indices (a device may repeat: two plans on one device),
- * or NULL for 0..n_dev-1.  Same cfg/seeds/out conventions and results as rl_optimize
- * (instances are independent); every cfg is checked before any device work.  The
- * calling thread's current device is unchanged on return. */
+ * or NULL for 0..n_dev-1.  Same cfg/seeds/out conventions as rl_optimize; every cfg is
+ * checked before any device work.  Every block runs the kernel shape rl_optimize picks for
+ * the whole batch B (rl_plan_set_shape_batch), so on devices with the same CU count the
+ * results equal rl_optimize's bit for bit, counters included (the shapes sum J and the
+ * lap in different tree orders).  The calling thread's current device is unchanged on
+ * return. */
 int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg,
                       const uint64_t* seeds, int32_t B, const int32_t* devices, int32_t n_dev,
                       rl_out* out_mincurv, rl_out* out_mintime);
@@ -219,6 +222,16 @@ int rl_plan_bind_device_outputs(rl_plan* plan, int32_t which, const rl_out* dev_
 /* device time of the last run, in ms, measured with HIP events on the run stream:
  * idx 0 = the whole run, 1 = the min-curvature kernel, 2 = the min-time kernel. */
 int rl_plan_kernel_ms(rl_plan* plan, int32_t idx, float* ms);
+/* The batch size the plan's kernel shape is chosen for (rl_kernel_shape's B); 0 = the plan's
+ * own B (the default).  Shapes differ in the tree order of the J / decrease / lap sums, so
+ * the last bits of J and the lap (and on a near-tie an Armijo decision) can depend on the
+ * shape: plans that must give identical results take the same shape batch.  Plans that run
+ * concurrently on one device should pass the total instance count in flight, so that none
+ * takes a latency shape meant to spread its instances over the whole GPU.  Takes effect
+ * at the next rl_plan_run. */
+int rl_plan_set_shape_batch(rl_plan* plan, int32_t shape_B);
+/* The kernel shape rl_plan_run launches for `mode` (K = 0: the streaming kernel). */
+int rl_plan_shape(rl_plan* plan, int32_t mode, int32_t* K, int32_t* T);
 int rl_plan_destroy(rl_plan* plan);
 
 /* B lap evaluations of given paths: heading/curvature
@@ -294,7 +307,9 @@ int rl_corridor(const rl_problem* prob, const rl_cfg* cfg, int32_t device, doubl
 int         rl_device_count(void);
 const char* rl_last_error(void);
 int         rl_abi_version(void);
-/* kernel variant the library would pick for N (samples per lane), or RL_ETOOBIG */
+/* samples per lane of the THROUGHPUT shape for N (4 or 8; 1 = the streaming kernel), or
+ * RL_ETOOBIG.  Batches small enough for a latency shape launch fewer samples per lane:
+ * rl_kernel_shape(N, B, mode) reports the shape a launch actually uses. */
 int         rl_kernel_variant(int32_t N);
 /* the kernel shape of a launch: *K samples per lane (0 = the streaming kernel) and *T lanes
  * per instance for N samples, a batch of B and mode RL_MODE_MINCURV or RL_MODE_MINTIME on

@@ -359,6 +359,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_plan_kernel_ms.restype = C.c_int
     lib.rl_plan_destroy.argtypes = [C.c_void_p]
     lib.rl_plan_destroy.restype = C.c_int
+    if hasattr(lib, "rl_plan_set_shape_batch"):   # absent only in older experiment builds (A/B bases)
+        lib.rl_plan_set_shape_batch.argtypes = [C.c_void_p, C.c_int32]
+        lib.rl_plan_set_shape_batch.restype = C.c_int
+        lib.rl_plan_shape.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.rl_plan_shape.restype = C.c_int
     lib.rl_device_count.restype = C.c_int
     lib.rl_last_error.restype = C.c_char_p
     lib.rl_abi_version.restype = C.c_int

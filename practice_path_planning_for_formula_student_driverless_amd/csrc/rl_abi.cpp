@@ -134,7 +134,7 @@ RingHost make_ring(const double* s, int E) {
     }
     // fp32 copies for the side filter (rl_corridor.h ring_rays): vertices, then block
     // circles with the radius rounded up; packed after the fp64 circles
-    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M + (size_t)4 * nb, 0.0f);
+    std::vector<float> f32((size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M, 0.0f);
     for (int v = 0; v < 2 * R.M; ++v) f32[v] = (float)R.vtx[v];
     for (int b = 0; b < nb; ++b) {
         float* o = &f32[(size_t)2 * R.M + (size_t)4 * b];
@@ -153,34 +153,6 @@ RingHost make_ring(const double* s, int E) {
         float hf = (float)hr;
         if ((double)hf < hr) hf = std::nextafter(hf, INFINITY);
         o[2] = hf;
-    }
-    // Direction cone per block (rl_corridor.h RL_ALONG): the smallest arc (mod pi) holding the
-    // directions of the segments that end in the block, as its unit centre (dx, dy) and
-    // s = sin(half width + 1e-3) + 1e-5 (fp32 evaluation margin); s = 2 (never "well
-    // conditioned") for an arc wider than pi/2 - 1e-3, a zero-length or non-finite segment
-    for (int b = 0; b < nb; ++b) {
-        float* o = &f32[(size_t)2 * R.M + (size_t)4 * nb + (size_t)4 * R.M + (size_t)4 * b];
-        std::vector<double> ang;
-        bool ok = true;
-        for (int v = b * rl::RL_BLK; v < (b + 1) * rl::RL_BLK; ++v) {
-            if (!ends[v]) continue;
-            const double vx = R.rec[v].vx, vy = R.rec[v].vy;
-            if (!std::isfinite(vx) || !std::isfinite(vy) || (vx == 0.0 && vy == 0.0)) { ok = false; break; }
-            double a = std::atan2(vy, vx);
-            a = std::fmod(a + 2 * M_PI, M_PI);
-            ang.push_back(a);
-        }
-        o[0] = 1.0f; o[1] = 0.0f; o[2] = 2.0f; o[3] = 0.0f;
-        if (!ok || ang.empty()) continue;
-        std::sort(ang.begin(), ang.end());
-        double gap = ang.front() + M_PI - ang.back(), start = ang.front();   // the wrap-around gap
-        for (size_t j = 1; j < ang.size(); ++j)
-            if (ang[j] - ang[j - 1] > gap) { gap = ang[j] - ang[j - 1]; start = ang[j]; }
-        const double half = 0.5 * (M_PI - gap), mid = start + half;
-        if (!(half + 1e-3 < 0.5 * M_PI - 1e-6)) continue;
-        o[0] = (float)std::cos(mid);
-        o[1] = (float)std::sin(mid);
-        o[2] = (float)(std::sin(half + 1e-3) + 1e-5);
     }
     const size_t n64 = R.blk.size();
     R.blk.resize(rl::ring_blk_doubles((size_t)R.M), 0.0);
@@ -220,6 +192,10 @@ int waves_per_instance(int N, int B, bool mintime, bool stream, int cus) {
 struct rl_plan {
     int device = 0;
     int N = 0, B = 0, modes = 0, ncfg = 0, max_outer = 0, closed = 1, Ei = 0, Eo = 0;
+    // batch size the kernel shape is chosen for (rl_plan_set_shape_batch; 0 = B): the
+    // shapes sum J and the lap in different orders, so plans whose results must equal
+    // each other's bit for bit use the same one (rl_optimize_multi: the whole call's B)
+    int shape_B = 0;
     bool stream = false;              // streaming kernel (use_stream at creation)
     double L = 0, veh_width = 0;
     hipStream_t own_stream = nullptr;
@@ -359,6 +335,23 @@ int rl_ring_segments(const double* ring_xy, int32_t n, int32_t closed, double* s
 }
 
 double rl_seed_value(uint64_t seed, int32_t i, double sigma) { return rl::seed_value(seed, i, sigma); }
+
+int rl_plan_set_shape_batch(rl_plan* plan, int32_t shape_B) {
+    if (!plan || shape_B < 0) return fail(RL_EINVAL, "rl_plan_set_shape_batch: bad argument");
+    plan->shape_B = shape_B;
+    return RL_OK;
+}
+
+int rl_plan_shape(rl_plan* plan, int32_t mode, int32_t* K, int32_t* T) {
+    if (!plan || !K || !T || (mode != RL_MODE_MINCURV && mode != RL_MODE_MINTIME))
+        return fail(RL_EINVAL, "rl_plan_shape: bad argument");
+    if (plan->stream) { *K = 0; *T = 1024; return RL_OK; }
+    const rl::Shape s = rl::pick_shape(std::max(plan->N, 1), plan->shape_B > 0 ? plan->shape_B : plan->B,
+                                       mode == RL_MODE_MINTIME, device_cus(plan->device));
+    *K = s.K;
+    *T = s.T;
+    return RL_OK;
+}
 
 int rl_plan_destroy(rl_plan* plan) {
     if (!plan) return RL_OK;
@@ -532,9 +525,10 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
     // the GPU with either kernel alone and run them one after the other (C3: concurrent
     // 74.2 ms vs 73.1 ms sequential).
     const int cus = device_cus(p->device);
+    const int sB = p->shape_B > 0 ? p->shape_B : p->B;
     const bool both = (p->modes & (RL_MODE_MINCURV | RL_MODE_MINTIME)) == (RL_MODE_MINCURV | RL_MODE_MINTIME) &&
-                      (int64_t)p->B * std::max(waves_per_instance(p->N, p->B, false, p->stream, cus),
-                                               waves_per_instance(p->N, p->B, true, p->stream, cus)) <=
+                      (int64_t)p->B * std::max(waves_per_instance(p->N, sB, false, p->stream, cus),
+                                               waves_per_instance(p->N, sB, true, p->stream, cus)) <=
                           (int64_t)8 * cus;
     if (both) HIPCHK(hipStreamWaitEvent(p->aux_stream, p->ev[0], 0));   // everything queued before the run
     for (int m = 0; m < 2; ++m) {
@@ -582,6 +576,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         kp.v = mb.v; kp.ax = mb.ax; kp.lap = mb.lap; kp.nx = mb.nx; kp.ny = mb.ny;
         kp.evals = mb.evals; kp.accepts = mb.accepts; kp.sweeps = mb.sweeps;
         kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
+        kp.shape_B = sB;
         kp.L = p->L; kp.veh_width = p->veh_width;
         HIPCHK(hipEventRecord(p->ev[1 + m], st));
         hipError_t e = p->stream ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
@@ -1321,9 +1316,11 @@ int rl_optimize_multi(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, 
     for (int d = 0; d < nb; ++d) {
         int b0, b1;
         block(d, b0, b1);
+        // every block takes the kernel shape rl_optimize would take for the whole batch, so
+        // the results equal rl_optimize's bit for bit (the shapes' J / lap sum orders differ)
         if ((rc = rl_plan_create(&plans[d], devs[d], prob, n_cfg == 1 ? cfg : cfg + b0, n_cfg == 1 ? 1 : b1 - b0,
                                  seeds ? seeds + b0 : nullptr, b1 - b0, modes)) ||
-            (rc = rl_plan_run(plans[d], nullptr)))
+            (rc = rl_plan_set_shape_batch(plans[d], B)) || (rc = rl_plan_run(plans[d], nullptr)))
             return release(rc);
     }
     auto shifted = [&](const rl_out* o, int b0, rl_out& s) -> rl_out* {

@@ -63,31 +63,15 @@ constexpr int RL_SUB = RL_BLK < 16 ? RL_BLK : 16;
 // a candidate word shifted past one skipped block
 __device__ __forceinline__ uint32_t shl_blk(uint32_t w) { return RL_BLK >= 32 ? 0u : (w << (RL_BLK & 31)); }
 // layout of RingDesc::blk: [M/B][4] fp64 circles, then fp32 vertices [M][2], fp32 circles
-// [M/B][4], fp32 midpoints [M][4] and fp32 direction cones [M/B][4] (counted in doubles)
+// [M/B][4] and fp32 midpoints [M][4] (counted in doubles)
 __host__ __device__ constexpr size_t ring_blk_off_vtx32(size_t M) { return 4 * M / RL_BLK; }
 __host__ __device__ constexpr size_t ring_blk_off_blk32(size_t M) { return 4 * M / RL_BLK + M; }
 __host__ __device__ constexpr size_t ring_blk_off_mid32(size_t M) { return 4 * M / RL_BLK + M + 2 * M / RL_BLK; }
-__host__ __device__ constexpr size_t ring_blk_off_cone32(size_t M) { return ring_blk_off_mid32(M) + 2 * M; }
-__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return ring_blk_off_cone32(M) + 2 * M / RL_BLK; }
+__host__ __device__ constexpr size_t ring_blk_doubles(size_t M) { return ring_blk_off_mid32(M) + 2 * M; }
 typedef __attribute__((address_space(4))) const float cflt;
 
-// Along-ray block culling (RL_ALONG).  A block the ray LINE crosses can still be skipped for
-// a sample when, along the ray, its circle lies behind the sample for +n and beyond the best
-// -n hit so far (or the other way round): no segment in it can then lower either minimum.
-// Exact when every segment of the block makes an angle of more than 1e-3 rad with the ray
-// (the host's direction cone per block: unit centre d and s = sin(half width + 1e-3) + 1e-5,
-// s = 2 when the cone is wider than pi/2 - 1e-3 or a segment has no direction).  Then the
-// reference's computed u and t are well conditioned: with |sin phi| >= 1e-3, a segment that
-// passes the u test crosses the ray line within (1e-12 + 1e-11)|v| of the segment, so the
-// crossing's exact parameter t* lies within R + 3e-11 of n.(C - P), and the computed t differs
-// from t* by at most 4u(|a| + |t*|) / |sin phi| + 2u|t| < 1e-12 (|a| + |t|): both far below
-// the fp32 margin m = R(1+1e-6) + 2 dl (dl >= 1e-6 (Rv + |q|_1), rl_abi.cpp make_ring) that
-// also covers the fp32 evaluation of n.(C - P).  The skipped segments could only have given
-// computed t >= the running minimum, which std::min-style `t < best` ignores.  Blocks are
-// scanned from the word nearest to the wave's first sample, so the near hit comes first.
-#ifndef RL_ALONG
-#define RL_ALONG 0
-#endif
+// (Along-ray block culling, round 4: built bit-exact with a per-block direction-cone guard and
+// measured slower on every configuration, then removed)
 
 // Block culling. Entries come in blocks of RL_BLK. The host gives each block a circle (C, R)
 // that contains both endpoints of every segment ending in the block (rl_abi.cpp
@@ -167,10 +151,6 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
     // the exact one and R is rounded up, so |c32(C)| > R(1+1e-6) + 2 dl32 leaves every
     // endpoint with |c32| > 2 dl32 - 11e(Rv+|q|_1) >= dl32 on the centre's side.
     float dl[CK], g[CK], uxf[CK], uyf[CK];
-#if RL_ALONG
-    float gA[CK];                          // n.P: the along-ray coordinate of the sample
-    cflt* CO = (cflt*)(R.blk + ring_blk_off_cone32(R.M));   // fp32 cones [M/B][4] (dx, dy, s, 0)
-#endif
 #pragma unroll
     for (int k = 0; k < CK; ++k) {
         const double q1 = fabs(qx[k]) + fabs(qy[k]);
@@ -178,9 +158,6 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
         dl[k] = (float)((R.dl0 + 4e-15 * q1) + (R.dl32 + 1e-6 * q1));
         uxf[k] = (float)ux[k];
         uyf[k] = (float)uy[k];
-#if RL_ALONG
-        gA[k] = (float)(ux[k] * qx[k] + uy[k] * qy[k]);
-#endif
         bp[k] = bn[k] = ub2[k] = INFINITY;
     }
     auto side = [&](int k, float vx, float vy) -> float { return __builtin_fmaf(uxf[k], vy, -__builtin_fmaf(uyf[k], vx, g[k])); };
@@ -199,62 +176,22 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
     }
     auto sgn = [](float x) -> uint32_t { return __float_as_uint(x) >> 31; };
     bool prev_ok = false;          // lp/lq hold the sides of the entry just before the next block
-    const int nwords = R.M / 32;
-    int w0 = 0;                    // first word of the scan
-#if RL_ALONG
-    {   // the word holding the block circle nearest to the wave's first sample (wave-uniform)
-        const float sx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)qx[0])));
-        const float sy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)qy[0])));
-        float best = INFINITY;
-        for (int b = 0; b < R.M / RL_BLK; ++b) {
-            cflt* bk = BK + 4 * b;
-            const float dx = bk[0] - sx, dy = bk[1] - sy;
-            const float d = sqrtf(__builtin_fmaf(dx, dx, dy * dy)) - bk[2];
-            if (bk[2] >= 0.0f && d < best) { best = d; w0 = b * RL_BLK / 32; }
-        }
-        w0 = __builtin_amdgcn_readfirstlane(w0);
-    }
-#endif
-    for (int wi = 0; wi < nwords; ++wi) {
-        const int b0 = ((w0 + wi) % nwords) * 32;
-        if (b0 == 0) prev_ok = false;        // the scan wrapped: the entry before is not the last one seen
+    for (int b0 = 0; b0 < R.M; b0 += 32) {
         uint32_t w[CK];
 #pragma unroll
         for (int k = 0; k < CK; ++k) w[k] = 0u;
         // which of the word's 32/RL_BLK blocks some lane's ray line may cross (wave-uniform)
         uint32_t visit = 0u;
-#if RL_ALONG
-        float bpf[CK], bnf[CK];             // the running minima, rounded up to fp32
-#pragma unroll
-        for (int k = 0; k < CK; ++k) {
-            bpf[k] = (float)(bp[k] * (1.0 + 1e-6));
-            bnf[k] = (float)(bn[k] * (1.0 + 1e-6));
-        }
-#endif
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
             cflt* bk = BK + 4 * ((b0 / RL_BLK) + q);
             const float cx = bk[0], cy = bk[1], rb = bk[2];
             bool need = false;
             if (rb >= 0.0f) {
-#if RL_ALONG
-                cflt* co = CO + 4 * ((b0 / RL_BLK) + q);
-                const float cdx = co[0], cdy = co[1], cs = co[2];
-#endif
 #pragma unroll
                 for (int k = 0; k < CK; ++k) {
                     const float c = side(k, cx, cy);
-                    bool nk = act[k] && !(fabsf(c) > rb * (1.0f + 1e-6f) + 2.0f * dl[k]);
-#if RL_ALONG
-                    if (nk && fabsf(__builtin_fmaf(uxf[k], cdy, -uyf[k] * cdx)) > cs) {
-                        const float a = __builtin_fmaf(uxf[k], cx, __builtin_fmaf(uyf[k], cy, -gA[k]));
-                        const float m = rb * (1.0f + 1e-6f) + 2.0f * dl[k];
-                        const bool plus_dead = (a + m < 0.0f) || (a - m > bpf[k]);
-                        const bool minus_dead = (a - m > 0.0f) || (-a - m > bnf[k]);
-                        nk = !(plus_dead && minus_dead);
-                    }
-#endif
-                    need |= nk;
+                    need |= act[k] && !(fabsf(c) > rb * (1.0f + 1e-6f) + 2.0f * dl[k]);
                 }
             }
             if (__any(need)) visit |= 1u << q;

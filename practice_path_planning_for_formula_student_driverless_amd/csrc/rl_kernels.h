@@ -23,6 +23,7 @@ struct KParams {
     double *nx, *ny;           // scratch normals [B][N]
     int32_t *evals, *accepts, *sweeps;
     int32_t N, Ei, Eo, ncfg, B, closed;
+    int32_t shape_B;           // batch size the kernel shape is chosen for (pick_shape; >= 1)
     int64_t center_stride;     // doubles between instances' centres (0: shared)
     double L, veh_width;
 };

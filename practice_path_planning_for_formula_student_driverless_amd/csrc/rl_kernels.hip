@@ -98,7 +98,7 @@ hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     constexpr bool CL = RL_ANALYZE_ONE != 2;
     return mintime ? launch_t<8, 256, CL, true>(p, st) : launch_t<8, 256, CL, false>(p, st);
 #else
-    const Shape s = pick_shape(p.N, p.B, mintime, cu_count());
+    const Shape s = pick_shape(p.N, p.shape_B > 0 ? p.shape_B : p.B, mintime, cu_count());
     const Shape lat = lat_shape(p.N);
     if ((s.K == lat.K && s.T == lat.T) || (s.K == 4 && s.T == 512)) return launch_optimize_lat(p, mintime, st);
     if (s.K == 4 && s.T == 64) return launch_kt<4, 64>(p, mintime, st);

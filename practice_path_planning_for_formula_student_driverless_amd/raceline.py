@@ -158,6 +158,17 @@ class Plan:
     def run(self, stream_ptr: int = 0) -> None:
         _check(_lib().rl_plan_run(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def set_shape_batch(self, shape_B: int) -> None:
+        """Choose the kernel shape for a batch of shape_B instances (0 = this plan's B):
+        rl_plan_set_shape_batch.  Concurrent plans on one device pass the total in flight."""
+        _check(_lib().rl_plan_set_shape_batch(self._h, int(shape_B)))
+
+    def shape(self, mode: int) -> tuple:
+        """(K, T) of the kernel rl_plan_run launches for `mode` (K = 0: streaming kernel)."""
+        k, t = C.c_int32(), C.c_int32()
+        _check(_lib().rl_plan_shape(self._h, int(mode), C.byref(k), C.byref(t)))
+        return k.value, t.value
+
     def kernel_ms(self, idx: int) -> float:
         ms = C.c_float()
         _check(_lib().rl_plan_kernel_ms(self._h, idx, C.byref(ms)))

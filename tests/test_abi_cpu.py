@@ -36,7 +36,7 @@ def test_header_declares_expected_entry_points():
                  "rl_ring_segments", "rl_seed_value", "rl_device_count", "rl_last_error", "rl_abi_version",
                  "rl_kernel_variant", "rl_geom", "rl_optimize_multi", "rl_lap_eval", "rl_corridor", "rl_format_csv",
                  "rl_last_call_ms", "rl_last_call_times", "rl_release_plan_cache", "rl_plan_cache_info",
-                 "rl_kernel_shape"):
+                 "rl_kernel_shape", "rl_plan_set_shape_batch", "rl_plan_shape"):
         assert must in names
 
 

@@ -728,6 +728,37 @@ def test_optimize_multi_equals_single(devices):
     assert ei.value.code == abi.RL_EINVAL
 
 
+def test_optimize_multi_straddling_shape_threshold_equals_single():
+    """rl_optimize_multi when the per-device block would pick a latency shape but the whole
+    batch a throughput shape: every block runs the whole batch's shape
+    (rl_plan_set_shape_batch), so every output, counters included, equals rl_optimize's
+    bit for bit.  Plan.shape reports the shape a plan launches."""
+    _lib_or_skip()
+    case = O.load_case("track_training_map")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    N = prob.N
+    B = next(b for b in range(4, 8192, 2)
+             if abi.kernel_shape(N, b // 2, abi.RL_MODE_MINCURV) != abi.kernel_shape(N, b, abi.RL_MODE_MINCURV))
+    assert abi.kernel_shape(N, B // 2, abi.RL_MODE_MINCURV)[0] < abi.kernel_shape(N, B, abi.RL_MODE_MINCURV)[0]
+    seeds = np.arange(B, dtype=np.uint64)
+    mc1, mt1 = raceline.optimize_batch(prob, cfg, seeds, B)
+    mc2, mt2 = raceline.optimize_batch(prob, cfg, seeds, B, devices=[0, 0])
+    for a, b in ((mc1, mc2), (mt1, mt2)):
+        for f in abi.OUT_F64 + ("evals", "accepts"):
+            np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    for f in ("v", "ax", "lap", "vpass_sweeps"):
+        np.testing.assert_array_equal(getattr(mt1, f), getattr(mt2, f), err_msg=f)
+    pl = raceline.Plan(prob, cfg, seeds=seeds[:B // 2], B=B // 2, modes=abi.RL_MODE_MINCURV)
+    assert pl.shape(abi.RL_MODE_MINCURV) == abi.kernel_shape(N, B // 2, abi.RL_MODE_MINCURV)
+    pl.set_shape_batch(B)
+    assert pl.shape(abi.RL_MODE_MINCURV) == abi.kernel_shape(N, B, abi.RL_MODE_MINCURV)
+    pl.run()
+    mc3, _ = pl.fetch()
+    pl.close()
+    for f in abi.OUT_F64 + ("evals", "accepts"):
+        np.testing.assert_array_equal(getattr(mc3, f), getattr(mc1, f)[:B // 2], err_msg=f)
+
+
 def test_dropin_plan_cache_reuse_is_exact():
     """rl_optimize's plan cache (the reference's one-call-per-track use): repeated calls
     with the same rings reuse the device plan and pinned staging; the centreline, cfg and
