@@ -55,7 +55,28 @@ struct VConst {
     double Fr;          // mass_kg*9.81*c_rr
     double mass, Pmax, acc_cap, brk_cap;
     double h, two_h;
+    int32_t pw_free;    // the power limit can never bind (see power_never_binds); read per step
+    int32_t _pad;
 };
+
+// True when the power limit of ax_max_at (ref:812-817) can never be the smallest of
+// std::min({a_res, a_long_acc_cap, a_power}) (ref:818) for any speed the v-pass produces,
+// so the forward step may skip its two divisions: every v of the profile is <= v_cap
+// (ref:787-794 caps the start values, every later value is a std::min with them), and for
+// 1e-6 < v <= v_cap the exact a_power(v) = P/(m v) - (kFd v^2 + Fr)/m is decreasing in v,
+// so a_power(v) >= a_power(v_cap).  The computed a_power differs from the exact one by a
+// few ulps of P/(m v) + (Fd + Fr)/m, far below the margin 1e-9 (1 + cap) required here, so
+// it stays strictly above acc_cap >= min(a_res, acc_cap), and std::min never picks it (a
+// NaN a_power is never picked either; v <= 1e-6 gives 1e9 > acc_cap).  The minimum is then
+// min(a_res, acc_cap) bit for bit.
+__device__ __forceinline__ bool power_never_binds(double Pmax, double mass, double kFd, double Fr, double v_cap,
+                                                  double acc_cap) {
+    if (!(Pmax > 0.0) || !(mass > 0.0) || !(v_cap > 1e-6) || !(kFd >= 0.0) || !(Fr >= 0.0)) return false;
+    if (!(Pmax < 1e300) || !(mass < 1e300) || !(v_cap < 1e150) || !(kFd < 1e300) || !(Fr < 1e300)) return false;
+    if (!(acc_cap < 1e8) || !(acc_cap > -1e300)) return false;
+    const double lb = Pmax / (mass * v_cap) - (kFd * v_cap * v_cap + Fr) / mass;
+    return lb > acc_cap + 1e-9 * (1.0 + fabs(acc_cap)) + 1e-9 * (Pmax / (mass * v_cap));
+}
 
 // IEEE maxNum / minNum on the fp64 VALU (one instruction each).  They equal the
 // reference's std::max(lo, x) / std::min(hi, x) select forms for every x unless a
@@ -108,16 +129,19 @@ __device__ __forceinline__ double vs_min(double a, double b) { return smin(a, b)
 __device__ __forceinline__ double vstep_fwd(const VConst& c, double vi, double ki) {
     double alat = vi * vi * fabs(ki);
     double a_res = sqrt(vs_max0(c.a_total2 - alat * alat));
-    double Fd = c.kFd * vi * vi;
+    double a_acc = vs_min(a_res, c.acc_cap);
+    if (!__builtin_amdgcn_readfirstlane(c.pw_free)) {   // uniform per instance (power_never_binds)
+        double Fd = c.kFd * vi * vi;
 #if RL_VSTEP_FAST
-    // evaluated unconditionally and selected: as the arm of a branch its two divisions ran
-    // after the a_res chain instead of beside it (a discarded value has no effect)
-    const double ap = c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass;
-    double a_power = (c.Pmax > 0 && vi > 1e-6) ? ap : 1e9;
+        // evaluated unconditionally and selected: as the arm of a branch its two divisions ran
+        // after the a_res chain instead of beside it (a discarded value has no effect)
+        const double ap = c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass;
+        double a_power = (c.Pmax > 0 && vi > 1e-6) ? ap : 1e9;
 #else
-    double a_power = (c.Pmax > 0 && vi > 1e-6) ? (c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass) : 1e9;
+        double a_power = (c.Pmax > 0 && vi > 1e-6) ? (c.Pmax / (c.mass * vi) - (Fd + c.Fr) / c.mass) : 1e9;
 #endif
-    double a_acc = vs_min(vs_min(a_res, c.acc_cap), a_power);   // std::min({a_res, cap, a_power}) ref:818
+        a_acc = vs_min(a_acc, a_power);     // std::min({a_res, cap, a_power}) ref:818
+    }
     a_acc = vs_max0(a_acc);
     return sqrt(vs_max0(__builtin_fma(2.0, a_acc * c.h, vi * vi)));   // 2*(a*h) is exact: the sum's one rounding
 }

@@ -219,7 +219,7 @@ __device__ __forceinline__ void put(double (&a)[K], int idx, double v) {
     }
 }
 
-template <int K, int T>
+template <int K, int T, bool MT>
 struct alignas(16) Smem {
     static constexpr int NW = T / 64;
     // The small tables come first: their (mostly wave-uniform) addresses then fit the
@@ -238,6 +238,10 @@ struct alignas(16) Smem {
     double bc[4];                // broadcast scalars
     int ctr;                     // corridor work queue: next chunk of 64*CK samples
     VConst vc;                   // v-pass constants (read per v pass: no registers held across the kernel)
+    // min-time: warm start of the v-pass relaxations, per thread the incoming value its chunk
+    // ended with in [0] the first forward sweep of the previous v pass, [1] the latest forward
+    // sweep, [2] / [3] the same for the backward sweeps (+inf: none yet; see vpass)
+    double vg[MT ? 4 : 1][MT ? T : 1];
     union {
         double2 coef[2][K][T];   // [0]: (A1,A2)  [1]: (N0,W)   (precompute_lin_geom_generic)
         double vin[2][T];        // v-pass relaxation: published outgoing values
@@ -315,7 +319,7 @@ struct MinWaves {
 template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
 __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_kernel(KParams p) {
     constexpr int NW = T / 64;
-    __shared__ Smem<K, T> sm;
+    __shared__ Smem<K, T, MT> sm;
 #ifdef RL_STAMPS
     unsigned long long st_acc[16] = {};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
@@ -390,8 +394,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     auto xpub = [&](int slot, const double (&a)[K]) RL_AI {
         if constexpr (NW == 1) return;       // one wave: xget reads the edges with readlane
         const double first = a[0], last = a[K - 1];
-        aF[slot * Smem<K, T>::RF] = first;
-        aL[slot * Smem<K, T>::RF] = last;
+        aF[slot * Smem<K, T, MT>::RF] = first;
+        aL[slot * Smem<K, T, MT>::RF] = last;
         if (!RAGGED || cntL == K) {
             aW[slot * 65] = last;
         } else if (part_wave) {
@@ -603,7 +607,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
         vc.acc_cap = vs_cap(C.a_long_acc_cap); vc.brk_cap = vs_cap(C.a_long_brake_cap);
         vc.h = h; vc.two_h = two_h;          // two_h = uni(2*h): the same value, from an SGPR pair
+        vc.pw_free = power_never_binds(C.P_max_W, C.mass_kg, vc.kFd, vc.Fr, C.v_cap_mps, vc.acc_cap);
         sm.vc = vc;          // first read after the outer loop's first barrier
+    }
+    if constexpr (MT) {      // v-pass warm starts: none yet (each thread reads only its own)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm.vg[j][tid] = INFINITY;
     }
 
     auto same_bits = [](double a, double b) RL_AI -> bool { return __double_as_longlong(a) == __double_as_longlong(b); };
@@ -635,17 +644,25 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             // bit, the one it already holds (each step depends only on the previous value), so
             // its outgoing value would repeat.  Each chunk's result is a deterministic function
             // of its incoming value, so the fixed point is the serial result bit for bit.
+            // Warm start: the first round takes as incoming value the one this chunk ended with
+            // in the same sweep of the previous v pass (sweep 0) or in the previous sweep (lane
+            // 0 also keeps it as the previous wave's value until that wave publishes).  Any
+            // start reaches the same fixed point -- chunk t is exact from round t on, and the
+            // rounds end only when every incoming value equals its neighbour's outgoing one --
+            // and a start that is already exact leaves nothing to re-evaluate.
             {
+                const double g = MT ? sm.vg[MT && s == 0 ? 0 : MT ? 1 : 0][MT ? tid : 0] : INFINITY;
                 double in_prev = -1.0;       // sentinel (valid values are >= 0 or +inf)
                 double out = INFINITY;       // the value this chunk passes right
-                double wave_in = INFINITY;   // lane 0: the previous wave's last outgoing value
+                double wave_in = g;          // lane 0: the previous wave's last outgoing value
                 double pub = -1.0;           // lane 63: the value last published for the next wave
                 bool first = true;
                 for (int ro = 0;; ++ro) {
                     bool conv = false;         // wave-uniform: the in-wave relaxation settled
                     for (int ir = 0; ir < VpRounds<K, T>::value; ++ir) {
                         double in = dpp_from_left_or(out, wave_in);
-                        if (first || !has_left) in = INFINITY;
+                        if (first) in = g;
+                        if (!has_left) in = INFINITY;
                         bool ch = false;
                         if (active && in != in_prev) {
                             in_prev = in;
@@ -682,6 +699,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid > 0) wave_in = sm.u.vin[ro & 1][wid - 1];
                 }
+                if constexpr (MT) {
+                    sm.vg[1][tid] = in_prev;
+                    if (s == 0) sm.vg[0][tid] = in_prev;
+                }
             }
             // closed wrap (ref:834-839): v[0] = min(v[0], f(v[N-1], k[N-1]))
             if (CLOSED) {
@@ -699,16 +720,18 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 double vpre[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) vpre[k] = v[k];
+                const double g = MT ? sm.vg[MT && s == 0 ? 2 : MT ? 3 : 0][MT ? tid : 0] : INFINITY;   // warm start (as forward)
                 double in_prev = -1.0;
                 double out = INFINITY;
-                double wave_in = INFINITY;   // lane 63: the next wave's first outgoing value
+                double wave_in = g;          // lane 63: the next wave's first outgoing value
                 double pub = -1.0;           // lane 0: the value last published for the previous wave
                 bool first = true;
                 for (int ro = 0;; ++ro) {
                     bool conv = false;         // wave-uniform: the in-wave relaxation settled
                     for (int ir = 0; ir < VpRounds<K, T>::value; ++ir) {
                         double in = dpp_from_right_or(out, wave_in);
-                        if (first || !has_right) in = INFINITY;
+                        if (first) in = g;
+                        if (!has_right) in = INFINITY;
                         bool ch = false;
                         if (active && in != in_prev) {
                             in_prev = in;
@@ -744,6 +767,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     }
                     if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid + 1 < NW) wave_in = sm.u.vin[ro & 1][wid + 1];
+                }
+                if constexpr (MT) {
+                    sm.vg[3][tid] = in_prev;
+                    if (s == 0) sm.vg[2][tid] = in_prev;
                 }
             }
             // closed wrap (ref:846-850): v[N-1] = min(v[N-1], b(v[0], k[0]))

@@ -88,6 +88,10 @@ constexpr int RED_SLOTS = 3 * RL_BT_BATCH > 4 ? 3 * RL_BT_BATCH : 4;
 struct SSmem {
     double red[RED_SLOTS][NWS];
     double vin[2][TS];
+    // warm start of the v-pass relaxations: per thread, the incoming value its chunk ended
+    // with in [0] the first forward sweep of the previous v pass, [1] the latest forward
+    // sweep, [2] / [3] the same for the backward sweeps (+inf: none yet)
+    double vg[4][TS];
     double bc[4];
     VConst vc;        // v-pass constants (read at the start of each v pass: no registers held)
     int ctr;          // corridor work queue: next chunk of 64*RL_SCK samples
@@ -295,8 +299,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
         vc.acc_cap = vs_cap(C.a_long_acc_cap); vc.brk_cap = vs_cap(C.a_long_brake_cap);
         vc.h = h; vc.two_h = two_h;      // two_h = uni(2*h): the same value, from an SGPR pair
+        vc.pw_free = power_never_binds(C.P_max_W, C.mass_kg, vc.kFd, vc.Fr, C.v_cap_mps, vc.acc_cap);
         sm.vc = vc;                      // first read after the outer loop's first barrier
     }
+    for (int j = 0; j < 4; ++j) sm.vg[j][tid] = INFINITY;   // own entries only, read by this thread
     const int Cr = (N + TS - 1) / TS;
     const int r0 = min(N, tid * Cr), r1 = min(N, r0 + Cr);
     const bool ract = r0 < r1;
@@ -314,11 +320,12 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             ++sweeps;
             for (int i = r0; i < r1; ++i) VS[i] = V[i];           // sweep start
             __syncthreads();
-            // forward (ref:829-833)
+            // forward (ref:829-833), warm-started (see vpass_reg)
             double in_prev = -1.0;
+            const double gf = sm.vg[s == 0 ? 0 : 1][tid];
             for (int it = 0;; ++it) {
                 double in = INFINITY;
-                if (it > 0 && has_left) in = sm.vin[(it - 1) & 1][tid - 1];
+                if (has_left) in = (it > 0) ? sm.vin[(it - 1) & 1][tid - 1] : gf;
                 bool changed = false;
                 if (ract && in != in_prev) {
                     changed = (it > 0);
@@ -335,6 +342,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 }
                 if (!__syncthreads_or(changed) && it > 0) break;
             }
+            if (has_left) {
+                sm.vg[1][tid] = in_prev;
+                if (s == 0) sm.vg[0][tid] = in_prev;
+            }
             if (CLOSED) {                                          // ref:834-839
                 if (ract && r1 == N) sm.bc[0] = vstep_fwd(vc, V[N - 1], KA[N - 1]);
                 __syncthreads();
@@ -345,9 +356,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             for (int i = r0; i < r1; ++i) Q1[i] = V[i];            // pass start (Q1 is free here)
             __syncthreads();
             in_prev = -1.0;
+            const double gb = sm.vg[s == 0 ? 2 : 3][tid];
             for (int it = 0;; ++it) {
                 double in = INFINITY;
-                if (it > 0 && has_right) in = sm.vin[(it - 1) & 1][tid + 1];
+                if (has_right) in = (it > 0) ? sm.vin[(it - 1) & 1][tid + 1] : gb;
                 bool changed = false;
                 if (ract && in != in_prev) {
                     changed = (it > 0);
@@ -363,6 +375,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
                 }
                 if (!__syncthreads_or(changed) && it > 0) break;
+            }
+            if (has_right) {
+                sm.vg[3][tid] = in_prev;
+                if (s == 0) sm.vg[2][tid] = in_prev;
             }
             if (CLOSED) {                                          // ref:846-850
                 if (tid == 0) sm.bc[1] = vstep_bwd(vc, V[0], KA[0]);
@@ -406,10 +422,16 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 double vst[CR];
 #pragma unroll
                 for (int k = 0; k < CR; ++k) vst[k] = v[k];
+                // warm start: round 0 takes the incoming value this chunk ended with in the
+                // same sweep of the previous v pass (sweep 0) or in the previous sweep; any
+                // start converges to the same fixed point (chunk t is exact from round t on,
+                // and the rounds end only when every input equals its neighbour's output),
+                // and a start that is already exact leaves nothing to re-evaluate
                 double in_prev = -1.0, out = INFINITY;
+                const double gf = sm.vg[s == 0 ? 0 : 1][tid];
                 for (int it = 0;; ++it) {
                     double in = INFINITY;
-                    if (it > 0 && has_left) in = sm.vin[(it - 1) & 1][tid - 1];
+                    if (has_left) in = (it > 0) ? sm.vin[(it - 1) & 1][tid - 1] : gf;
                     bool ch = false;
                     if (ract && in != in_prev) {
                         in_prev = in;
@@ -433,7 +455,14 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         }
                     }
                     if (has_right) sm.vin[it & 1][tid] = out;
+#ifdef RL_STAMPS
+                    st_acc[12] += 1;
+#endif
                     if (!__syncthreads_or(ch) && it > 0) break;
+                }
+                if (has_left) {
+                    sm.vg[1][tid] = in_prev;
+                    if (s == 0) sm.vg[0][tid] = in_prev;
                 }
                 if (CLOSED) {                                  // ref:834-839
                     if (ract && r1 == N) {
@@ -455,9 +484,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 for (int k = 0; k < CR; ++k) vpre[k] = v[k];
                 __syncthreads();                               // vin reuse: the forward reads are done
                 double in_prev = -1.0, out = INFINITY;
+                const double gb = sm.vg[s == 0 ? 2 : 3][tid];
                 for (int it = 0;; ++it) {
                     double in = INFINITY;
-                    if (it > 0 && has_right) in = sm.vin[(it - 1) & 1][tid + 1];
+                    if (has_right) in = (it > 0) ? sm.vin[(it - 1) & 1][tid + 1] : gb;
                     bool ch = false;
                     if (ract && in != in_prev) {
                         in_prev = in;
@@ -481,7 +511,14 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         }
                     }
                     if (has_left) sm.vin[it & 1][tid] = out;
+#ifdef RL_STAMPS
+                    st_acc[13] += 1;
+#endif
                     if (!__syncthreads_or(ch) && it > 0) break;
+                }
+                if (has_right) {
+                    sm.vg[3][tid] = in_prev;
+                    if (s == 0) sm.vg[2][tid] = in_prev;
                 }
                 if (CLOSED) {                                  // ref:846-850
                     if (tid == 0) sm.bc[1] = vstep_bwd(vc, v[0], ka[0]);
@@ -606,6 +643,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         }
         if (MT) {
             const int sw = vpass_any();                            // ref:947 / 1047
+            RL_SSTAMP(11);
+#ifdef RL_STAMPS
+            st_acc[14] += sw;                                      // (counts, not cycles)
+#endif
             if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
             __syncthreads();
             if (outer == MO) {
