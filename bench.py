@@ -364,10 +364,17 @@ def run_c4(world, rank, local, dev, dist):
     base = load_problem("track_training_map")[2]
     cfgs = D.c4_cfgs(base)
     plans, mt_plans, meta = [], [], []
+    n_flight = sum(len(ks) for ks in groups.values())     # instances of all concurrent plans
+    shapes = {}
     for t, ks in groups.items():
         case, prob, _ = load_problem("track_" + D.C4_TRACKS[t])
         for mode in (abi.RL_MODE_MINCURV, abi.RL_MODE_MINTIME):
             pl = raceline.Plan(prob, [cfgs[k] for k in ks], B=len(ks), modes=mode, device=local)
+            # the plans run concurrently: every one takes the shape of the whole rank's load
+            # (ADVICE r4), not a latency shape meant to spread its own few instances over the GPU
+            pl.set_shape_batch(n_flight)
+            shapes.setdefault(D.C4_TRACKS[t], {})["mincurv" if mode == abi.RL_MODE_MINCURV else "mintime"] = \
+                "x".join(map(str, pl.shape(mode)))
             plans.append(pl)
             if mode == abi.RL_MODE_MINTIME:
                 mt_plans.append(pl)
@@ -401,6 +408,7 @@ def run_c4(world, rank, local, dev, dist):
         allst = allst.cpu().numpy()
         dt, n_inst = float(allst[:, 0].max()), int(allst[:, 1].sum())
     return {"instances": int(n_inst), "modes": "min-curv + min-time", "ms": round(dt * 1e3, 3),
+            "rank0_plan_shapes_KxT": shapes, "shape_batch": n_flight,
             "tracks_per_s": round(n_inst / dt, 1), "outer_iters_per_s": round(2 * 14 * n_inst / dt, 1),
             "lap_min_s": float(laps.min()), "lap_max_s": float(laps.max())}, laps
 

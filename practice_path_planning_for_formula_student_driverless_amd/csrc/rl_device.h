@@ -59,6 +59,21 @@ struct VConst {
     int32_t _pad;
 };
 
+#ifndef RL_VC_UNI
+#define RL_VC_UNI 1      // v-pass constants in SGPRs (A/B knob)
+#endif
+// the v-pass constants as wave-uniform values (SGPR pairs) rather than per-lane VGPR copies
+// of the LDS table: the register-resident relaxations hold 3 x Cr doubles per lane already
+__device__ __forceinline__ VConst vconst_uniform(const VConst& s) {
+    VConst c;
+    c.a_total = uni(s.a_total); c.a_total2 = uni(s.a_total2); c.kFd = uni(s.kFd); c.Fr = uni(s.Fr);
+    c.mass = uni(s.mass); c.Pmax = uni(s.Pmax); c.acc_cap = uni(s.acc_cap); c.brk_cap = uni(s.brk_cap);
+    c.h = uni(s.h); c.two_h = uni(s.two_h);
+    c.pw_free = __builtin_amdgcn_readfirstlane(s.pw_free);
+    c._pad = 0;
+    return c;
+}
+
 // True when the power limit of ax_max_at (ref:812-817) can never be the smallest of
 // std::min({a_res, a_long_acc_cap, a_power}) (ref:818) for any speed the v-pass produces,
 // so the forward step may skip its two divisions: every v of the profile is <= v_cap

@@ -618,7 +618,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     auto same_bits = [](double a, double b) RL_AI -> bool { return __double_as_longlong(a) == __double_as_longlong(b); };
     // returns sweeps executed; padding samples hold ka=0, v=+inf (never bind)
     auto vpass = [&](const double (&ka)[K], double (&v)[K]) RL_AI -> int {
-        const VConst vc = sm.vc;
+        const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double kk = fabs(ka[k]);

@@ -83,11 +83,29 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 #ifndef RL_BT_BATCH
 #define RL_BT_BATCH 4
 #endif
+#ifndef RL_BT_FIRST_MT
+#define RL_BT_FIRST_MT 0 // min-time: the first trial joins a batch as well (A/B knob)
+#endif
+// adaptive first trial: it joins a batch exactly when the instance's previous first trial was
+// rejected (the all-rejected regime of C5, E_k = 21), and is evaluated alone otherwise (the
+// accepting regime, where a batch's three extra steps are wasted work).  Uniform per
+// instance; exact either way (a batched step is bit-identical to a lone trial).
+#ifndef RL_BT_ADAPT
+#define RL_BT_ADAPT 1
+#endif
 constexpr int RED_SLOTS = 3 * RL_BT_BATCH > 4 ? 3 * RL_BT_BATCH : 4;
 
+// corridor ray scans: the work-list form of rl_corridor.h (each lane's samples test only
+// their own blocks), RL_SWL = 0 keeps the wave-union scan (A/B knob)
+#ifndef RL_SWL
+#define RL_SWL 0
+#endif
 struct SSmem {
     double red[RED_SLOTS][NWS];
-    double vin[2][TS];
+    union {
+        double vin[2][TS];             // v-pass relaxation (the corridor phase is over by then)
+        WlScratch<RL_SCK> wl[NWS];     // corridor work lists, one per wave
+    } u;
     // warm start of the v-pass relaxations: per thread, the incoming value its chunk ended
     // with in [0] the first forward sweep of the previous v pass, [1] the latest forward
     // sweep, [2] / [3] the same for the backward sweeps (+inf: none yet)
@@ -310,7 +328,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     // (A/B, round 3: the register kernel's in-wave DPP relaxation made this kernel's C5
     // min-time run 5-15 % slower at every round cap tried -- one barrier per round stays)
     auto vpass = [&]() -> int {
-        const VConst vc = sm.vc;
+        const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
         for (int i = r0; i < r1; ++i) {
             double kk = fabs(KA[i]);
             V[i] = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
@@ -325,7 +343,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             const double gf = sm.vg[s == 0 ? 0 : 1][tid];
             for (int it = 0;; ++it) {
                 double in = INFINITY;
-                if (has_left) in = (it > 0) ? sm.vin[(it - 1) & 1][tid - 1] : gf;
+                if (has_left) in = (it > 0) ? sm.u.vin[(it - 1) & 1][tid - 1] : gf;
                 bool changed = false;
                 if (ract && in != in_prev) {
                     changed = (it > 0);
@@ -336,9 +354,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
                         V[i + 1] = cur;
                     }
-                    if (has_right) sm.vin[it & 1][tid] = vstep_fwd(vc, cur, KA[r1 - 1]);
+                    if (has_right) sm.u.vin[it & 1][tid] = vstep_fwd(vc, cur, KA[r1 - 1]);
                 } else if (has_right) {
-                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
+                    sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
                 }
                 if (!__syncthreads_or(changed) && it > 0) break;
             }
@@ -359,7 +377,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             const double gb = sm.vg[s == 0 ? 2 : 3][tid];
             for (int it = 0;; ++it) {
                 double in = INFINITY;
-                if (has_right) in = (it > 0) ? sm.vin[(it - 1) & 1][tid + 1] : gb;
+                if (has_right) in = (it > 0) ? sm.u.vin[(it - 1) & 1][tid + 1] : gb;
                 bool changed = false;
                 if (ract && in != in_prev) {
                     changed = (it > 0);
@@ -370,9 +388,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
                         V[i] = cur;
                     }
-                    if (has_left) sm.vin[it & 1][tid] = vstep_bwd(vc, cur, KA[r0]);
+                    if (has_left) sm.u.vin[it & 1][tid] = vstep_bwd(vc, cur, KA[r0]);
                 } else if (has_left) {
-                    sm.vin[it & 1][tid] = sm.vin[(it - 1) & 1][tid];
+                    sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
                 }
                 if (!__syncthreads_or(changed) && it > 0) break;
             }
@@ -403,7 +421,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     auto same_bits = [](double a, double b) -> bool { return __double_as_longlong(a) == __double_as_longlong(b); };
     auto vpass_reg = [&](auto crc) -> int {
         constexpr int CR = decltype(crc)::value;
-        const VConst vc = sm.vc;
+        const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
         const int cnt = r1 - r0;                  // CR, except the last active thread; 0 beyond N
         double ka[CR], v[CR];
 #pragma unroll
@@ -415,6 +433,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             v[k] = (k < cnt) ? vk : INFINITY;
         }
         int sweeps = 0;
+        RL_SSTAMP(15);
         for (int s = 0; s < C.max_vpass_iters; ++s) {
             ++sweeps;
             bool any = false;
@@ -431,7 +450,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 const double gf = sm.vg[s == 0 ? 0 : 1][tid];
                 for (int it = 0;; ++it) {
                     double in = INFINITY;
-                    if (has_left) in = (it > 0) ? sm.vin[(it - 1) & 1][tid - 1] : gf;
+                    if (has_left) in = (it > 0) ? sm.u.vin[(it - 1) & 1][tid - 1] : gf;
                     bool ch = false;
                     if (ract && in != in_prev) {
                         in_prev = in;
@@ -454,12 +473,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                             out = o;
                         }
                     }
-                    if (has_right) sm.vin[it & 1][tid] = out;
-#ifdef RL_STAMPS
-                    st_acc[12] += 1;
-#endif
+                    if (has_right) sm.u.vin[it & 1][tid] = out;
                     if (!__syncthreads_or(ch) && it > 0) break;
                 }
+                RL_SSTAMP(12);
                 if (has_left) {
                     sm.vg[1][tid] = in_prev;
                     if (s == 0) sm.vg[0][tid] = in_prev;
@@ -483,11 +500,12 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
 #pragma unroll
                 for (int k = 0; k < CR; ++k) vpre[k] = v[k];
                 __syncthreads();                               // vin reuse: the forward reads are done
+                RL_SSTAMP(14);
                 double in_prev = -1.0, out = INFINITY;
                 const double gb = sm.vg[s == 0 ? 2 : 3][tid];
                 for (int it = 0;; ++it) {
                     double in = INFINITY;
-                    if (has_right) in = (it > 0) ? sm.vin[(it - 1) & 1][tid + 1] : gb;
+                    if (has_right) in = (it > 0) ? sm.u.vin[(it - 1) & 1][tid + 1] : gb;
                     bool ch = false;
                     if (ract && in != in_prev) {
                         in_prev = in;
@@ -510,12 +528,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                             out = o;
                         }
                     }
-                    if (has_left) sm.vin[it & 1][tid] = out;
-#ifdef RL_STAMPS
-                    st_acc[13] += 1;
-#endif
+                    if (has_left) sm.u.vin[it & 1][tid] = out;
                     if (!__syncthreads_or(ch) && it > 0) break;
                 }
+                RL_SSTAMP(13);
                 if (has_right) {
                     sm.vg[3][tid] = in_prev;
                     if (s == 0) sm.vg[2][tid] = in_prev;
@@ -533,7 +549,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 for (int k = 0; k < CR; ++k) any |= (k < cnt) && (v[k] != vpre[k]);
             }
             if (!__syncthreads_or(any)) break;                 // later sweeps are exact repeats
+            RL_SSTAMP(14);
         }
+        RL_SSTAMP(14);
 #pragma unroll
         for (int k = 0; k < CR; ++k)
             if (k < cnt) V[r0 + k] = v[k];
@@ -559,6 +577,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0;   // (the gradient needs no zeroing: each outer
     }                                                     // iteration's first evaluation writes it first)
     const int MO = C.max_outer_iters;
+    bool first_batch = RL_BT_ADAPT ? false : (RL_BT_FIRST && (!MT || RL_BT_FIRST_MT));
     double* al_p = AL;
     double* an_p = AN;
     RL_SSTAMP(0);
@@ -602,12 +621,24 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                     act[k] = i0 + k < N;
                 }
+#if RL_SWL
+                const WlSamples smp{X, Y, NX, NY, c * 64 * RL_SCK};
+#endif
 #ifdef RL_STAMPS
                 RL_SSTAMP(7);
+#if RL_SWL
+                corridor_bounds_wl<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk, smp, sm.u.wl[wid],
+                                           [&](int s) { RL_SSTAMP(s); });
+#else
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk,
                                         [&](int s) { RL_SSTAMP(s); });
+#endif
+#else
+#if RL_SWL
+                corridor_bounds_wl<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk, smp, sm.u.wl[wid]);
 #else
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
+#endif
 #endif
 #pragma unroll
                 for (int k = 0; k < RL_SCK; ++k) {
@@ -644,9 +675,6 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         if (MT) {
             const int sw = vpass_any();                            // ref:947 / 1047
             RL_SSTAMP(11);
-#ifdef RL_STAMPS
-            st_acc[14] += sw;                                      // (counts, not cycles)
-#endif
             if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
             __syncthreads();
             if (outer == MO) {
@@ -830,9 +858,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             bool accepted = false;
             int bt = 0;
             while (bt < 20) {
-                // (the first trial joins a batch for min-curv only: A/B, C5 27.8 -> 26.4 ms;
-                // min-time, with its higher register pressure, 67.2 -> 69.8 ms)
-                if (MB > 1 && ((RL_BT_FIRST && !MT) || bt > 0)) {
+                // (fixed rules measured before RL_BT_ADAPT: the first trial in a batch for min-curv
+                // only, C5 27.8 -> 26.4 ms; min-time 67.2 -> 69.8 ms)
+                if (MB > 1 && (first_batch || bt > 0)) {
                     const bool kept = bt == 0;             // step 0's vectors are stored by the pass
                     // the steps ref:737-740 would try next: halve, stop at 20 backtracks
                     // or below step_min
@@ -849,6 +877,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     bool stop = false;
                     for (int j = 0; j < m; ++j) {
                         ++evals;
+                        if (RL_BT_ADAPT && kept && j == 0) first_batch = !(Jn[0] <= J + C.armijo_c * dn[0]);
                         if (Jn[j] <= J + C.armijo_c * dn[j]) {
                             if (!(kept && j == 0)) materialize(st[j]);
                             double* t = al_p; al_p = an_p; an_p = t;
@@ -871,6 +900,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 const bool keep = (bt == 0);
                 const double Jn = eval_trial(step, keep, dec);
                 ++evals;
+                if (RL_BT_ADAPT && keep) first_batch = !(Jn <= J + C.armijo_c * dec);
                 if (Jn <= J + C.armijo_c * dec) {
                     if (!keep) materialize(step);
                     double* t = al_p; al_p = an_p; an_p = t;       // α := α_trial (uniform swap)

@@ -63,6 +63,8 @@ VARIANTS = {
     "stream_maxocc": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]}},
     # (iterative-ilp on rl_kernels.hip crashes this LLVM's register allocator on <8,256,closed,mintime>)
     "stream_iilp": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}},
+    "btfmt": {"RL_BT_FIRST_MT": 1, "RL_BT_ADAPT": 0},
+    "btfixed": {"RL_BT_ADAPT": 0},
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "stamps_eval": {"RL_STAMPS": 1, "RL_STAMPS_EVAL": 1},   # + the latency evaluation's phases (scripts/stamps_lat.py)
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed

@@ -1,7 +1,7 @@
 """C5 streaming-kernel phase shares with the v-pass split out (RL_STAMPS build,
-_lib/variants/librl_stamps.so): slot 11 = curvature + v-pass, slot 2 = gamma^2, and the
-v-pass counters (slot 12/13 = forward/backward relaxation rounds, 14 = sweeps) summed over
-the launch's calls.  Shares only: a stamped build's time is not the real kernel's.
+_lib/variants/librl_stamps.so): the v-pass split into its
+phases (register-resident v-pass: 15 load + v_kappa, 12 forward, 13 backward relaxations, 14
+wraps and sweep checks, 11 the stores), slot 2 = gamma^2.  Shares only: a stamped build's time is not the real kernel's.
 usage: stamps_c5v.py [B] [mode] [seed0]"""
 import ctypes as C, os, sys, numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -9,7 +9,8 @@ sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "tests"))
 import oracle_lib as O
 from practice_path_planning_for_formula_student_driverless_amd import abi
 lib = abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_stamps.so"))
-names = {0: "setup", 1: "corridor tail (write, seed)", 11: "mt: kappa + v-pass", 2: "mt: gamma^2 (+ lap)", 3: "lin-geom",
+names = {0: "setup", 1: "corridor tail (write, seed)", 15: "v-pass: load kappa, v_kappa", 12: "v-pass: forward relaxations",
+         13: "v-pass: backward relaxations", 14: "v-pass: wraps, sweep checks", 11: "v-pass: store", 2: "mt: gamma^2 (+ lap)", 3: "lin-geom",
          4: "PGD loop", 5: "update", 6: "normals", 7: "corridor loads", 8: "corridor: inner-ring rays",
          9: "corridor: outer-ring rays", 10: "corridor: fallback search"}
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
@@ -29,6 +30,4 @@ cyc = sum(tot[i] for i in names)
 print(f"C5 mode={MODE} B={B} seeds {S0}.. kernel {ms.value:.2f} ms; per-block cycles {cyc/B:.3e}")
 for i, nm in names.items():
     if tot[i] > 0: print(f"   {nm:30s} {100*tot[i]/cyc:5.1f}%  {tot[i]/B:.3e} cyc/block")
-print(f"   per block: forward rounds {tot[12]/B:.1f}, backward rounds {tot[13]/B:.1f}, sweeps {tot[14]/B:.2f} "
-      f"(over {cfg.max_outer_iters + 1} v-pass calls)")
 lib.rl_plan_destroy(h)
