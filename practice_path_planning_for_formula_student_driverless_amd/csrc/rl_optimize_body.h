@@ -547,8 +547,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // the block culling of rl_corridor.h skips most of both rings. The bounds reach their
     // owner threads through LDS, in the coefficient area, which is free until lin-geom
     // fills it: slot k*T+t holds (lo, hi) of sample t*K+k.
-    auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
-        constexpr int CKK = CK < K ? CK : K;
+    constexpr int CKK = CK < K ? CK : K;
+    // the scan (no barrier): the chunks of the work queue, bounds into the coefficient area
+    auto corridor_scan = [&](double guard) RL_AI {
         double2* bnd = &sm.u.coef[0][0][0];
         // Several waves: chunks of 64*CKK samples from a work queue in LDS, so a wave whose
         // rays are cheap takes the next chunk instead of waiting at the barrier below for
@@ -583,6 +584,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 if (act[k]) bnd[(i % K) * T + i / K] = make_double2(lc[k], hc[k]);
             }
         }
+    };
+    // every thread's own bounds (and its ghost samples') from the coefficient area
+    auto corridor_collect = [&](double (&lo)[K], double (&hi)[K]) RL_AI {
+        const double2* bnd = &sm.u.coef[0][0][0];
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -595,6 +600,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             loL = vl.x; hiL = vl.y; loR = vr.x; hiR = vr.y;
         }
         __syncthreads();      // the area is written again (v-pass relaxation, coefficients)
+    };
+    auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
+        corridor_scan(guard);
+        corridor_collect(lo, hi);
     };
 
     // ---- v(s) profile: velocity_profile_forward_backward ref:782-862 ---------
@@ -788,6 +797,136 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             for (int k = 0; k < K; ++k) any_change |= (k < cnt) && (v[k] != vstart[k]);
             if (!__syncthreads_or(any_change)) break;   // later sweeps are exact repeats
         }
+        return sweeps;
+    };
+
+    // ---- min-time latency shapes (K = 1, several waves): the v-pass on one wave -------
+    // VSPLIT: the v-pass (ref:782-862) runs on the last wave while the other waves scan the
+    // corridor (the two are independent: both need only the updated path), so a one-instance
+    // launch pays the longer of the two instead of their sum.  The v-pass wave holds KP = T/64
+    // consecutive samples per lane and relaxes them within the wave (DPP only, no barrier),
+    // with the warm start and early stops of `vpass`; curvature in and speeds out go through
+    // LDS (vsv).  Same fixed point, so the same values bit for bit.
+#ifndef RL_VSPLIT
+#define RL_VSPLIT 1
+#endif
+    constexpr bool VSPLIT = RL_VSPLIT && MT && K == 1 && NW >= 2 && T <= 512;
+    constexpr int KP = VSPLIT ? T / 64 : 1;
+    __shared__ double vsv[VSPLIT ? T : 1];
+    double vwg[4] = {INFINITY, INFINITY, INFINITY, INFINITY};   // warm starts (the v-pass wave's lanes)
+    auto vpass1w = [&]() RL_AI -> int {
+        const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
+        const int b0 = lane * KP;
+        const int c1 = min(KP, max(0, N - b0));
+        double ka1[KP], v[KP];
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+            ka1[j] = (j < c1) ? vsv[b0 + j] : 0.0;
+            const double kk = fabs(ka1[j]);
+            const double v_kappa = sqrt(C.a_lat_max / smax(kk, C.kappa_eps));
+            v[j] = (j < c1) ? smin(C.v_cap_mps, v_kappa) : INFINITY;   // ref:787-794
+        }
+        const bool act1 = c1 > 0, hasL = act1 && b0 > 0, hasR = act1 && b0 + c1 < N;
+        const int lastl = (N - 1) / KP;                 // the lane holding sample N-1
+        const int iters = C.max_vpass_iters;
+        int sweeps = 0;
+        for (int s = 0; s < iters; ++s) {
+            ++sweeps;
+            double vstart[KP];
+#pragma unroll
+            for (int j = 0; j < KP; ++j) vstart[j] = v[j];
+            {   // forward (ref:829-833)
+                const double g = vwg[s == 0 ? 0 : 1];
+                double in_prev = -1.0, out = INFINITY;
+                bool first = true;
+                for (;;) {
+                    double in = dpp_from_left_or(out, INFINITY);
+                    if (first) in = g;
+                    if (!hasL) in = INFINITY;
+                    bool ch = false;
+                    if (act1 && in != in_prev) {
+                        in_prev = in;
+                        double cur = vstart[0];
+                        if (hasL) cur = smin(vstart[0], in);
+                        bool go = first || !same_bits(cur, v[0]);
+                        v[0] = cur;
+#pragma unroll
+                        for (int j = 0; j + 1 < KP; ++j) {
+                            if (!__any(go)) break;
+                            if (go) {
+                                const double vf = vstep_fwd(vc, v[j], ka1[j]);
+                                const double nv = (j + 1 < c1) ? smin(vstart[j + 1], vf) : INFINITY;
+                                go = first || !same_bits(nv, v[j + 1]);
+                                v[j + 1] = nv;
+                            }
+                        }
+                        if (hasR && go) {                     // hasR => full chunk
+                            const double o = vstep_fwd(vc, v[KP - 1], ka1[KP - 1]);
+                            ch = o != out;
+                            out = o;
+                        }
+                    }
+                    if (first) { first = false; continue; }
+                    if (!__any(ch)) break;
+                }
+                vwg[1] = in_prev;
+                if (s == 0) vwg[0] = in_prev;
+            }
+            if (CLOSED) {                                     // ref:834-839
+                const double f = readlane(vstep_fwd(vc, pick(v, c1 - 1), pick(ka1, c1 - 1)), lastl);
+                if (lane == 0) v[0] = smin(v[0], f);
+            }
+            {   // backward (ref:841-845)
+                double vpre[KP];
+#pragma unroll
+                for (int j = 0; j < KP; ++j) vpre[j] = v[j];
+                const double g = vwg[s == 0 ? 2 : 3];
+                double in_prev = -1.0, out = INFINITY;
+                bool first = true;
+                for (;;) {
+                    double in = dpp_from_right_or(out, INFINITY);
+                    if (first) in = g;
+                    if (!hasR) in = INFINITY;
+                    bool ch = false;
+                    if (act1 && in != in_prev) {
+                        in_prev = in;
+                        const double cur = hasR ? smin(vpre[KP - 1], in) : vpre[KP - 1];
+                        bool go = first || !same_bits(cur, v[KP - 1]);
+                        v[KP - 1] = cur;
+#pragma unroll
+                        for (int j = KP - 2; j >= 0; --j) {
+                            if (!__any(go)) break;
+                            if (go) {
+                                const double vb = vstep_bwd(vc, v[j + 1], ka1[j + 1]);
+                                const double nv = (j < c1) ? smin(vpre[j], vb) : INFINITY;
+                                go = first || !same_bits(nv, v[j]);
+                                v[j] = nv;
+                            }
+                        }
+                        if (hasL && go) {
+                            const double o = vstep_bwd(vc, v[0], ka1[0]);
+                            ch = o != out;
+                            out = o;
+                        }
+                    }
+                    if (first) { first = false; continue; }
+                    if (!__any(ch)) break;
+                }
+                vwg[3] = in_prev;
+                if (s == 0) vwg[2] = in_prev;
+            }
+            if (CLOSED) {                                     // ref:846-850
+                const double f = readlane(vstep_bwd(vc, v[0], ka1[0]), 0);
+                if (lane == lastl) put(v, c1 - 1, smin(pick(v, c1 - 1), f));
+            }
+            bool any_change = false;
+#pragma unroll
+            for (int j = 0; j < KP; ++j) any_change |= (j < c1) && (v[j] != vstart[j]);
+            if (!__any(any_change)) break;                    // later sweeps are exact repeats
+        }
+#pragma unroll
+        for (int j = 0; j < KP; ++j)
+            if (j < c1) vsv[b0 + j] = v[j];
         return sweeps;
     };
 
@@ -1116,15 +1255,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         cL = cR = gL = gR = 0.0;
         __syncthreads();
         RL_STAMP(5);
-        if (outer < MO) {
-            // normals + corridor (ref:692-711 initially with the veh_width argument,
-            // ref:746-756 after each update with cfg veh_width_m)
-            if (tid == 0) sm.ctr = 0;                            // read after the barrier below
-            normals();
-            __syncthreads();
-            const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
-            corridor(guard, lo, hi);
-            if (outer == 0 && seed != 0) {                      // ref:720 + seed
+        // ref:720 + seed: the first outer iteration starts from the seeded alpha
+        auto seed_alpha = [&]() RL_AI {
+            if (outer == 0 && seed != 0) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     // (opaque: keeps the seed values from being hoisted out of the outer
@@ -1136,6 +1269,18 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     cL = smin(hiL, smax(loL, seed_value(seed, jl1, RL_SEED_SIGMA)));
                     cR = smin(hiR, smax(loR, seed_value(seed, jr1, RL_SEED_SIGMA)));
                 }
+            }
+        };
+        const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
+        if (outer < MO) {
+            // normals + corridor (ref:692-711 initially with the veh_width argument,
+            // ref:746-756 after each update with cfg veh_width_m)
+            if (tid == 0) sm.ctr = 0;                            // read after the barrier below
+            normals();
+            __syncthreads();
+            if constexpr (!VSPLIT) {                             // (VSPLIT: beside the v-pass below)
+                corridor(guard, lo, hi);
+                seed_alpha();
             }
         }
         RL_STAMP(1);
@@ -1164,8 +1309,28 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
         if (MT) {
             double v[K];
-            int sw = vpass(ka, v);                               // ref:947 / 1047
-            if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
+            if constexpr (VSPLIT) {
+                // the v-pass on the last wave, the corridor on the others, then both results
+                // reach their owners through LDS
+                vsv[tid] = ka[0];
+                __syncthreads();
+                if (wid_u == NW - 1) {
+                    const int sw = vpass1w();                    // ref:947 / 1047
+                    if (lane == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
+                } else if (outer < MO) {
+                    corridor_scan(guard);
+                }
+                if (outer < MO) {
+                    corridor_collect(lo, hi);                    // (its first barrier joins the two)
+                    seed_alpha();
+                } else {
+                    __syncthreads();
+                }
+                v[0] = active ? vsv[tid] : INFINITY;
+            } else {
+                const int sw = vpass(ka, v);                     // ref:947 / 1047
+                if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
+            }
             if (outer == MO) {
                 // ax and lap time (ref:854-860)
                 double lv, rv;
