@@ -277,217 +277,9 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Work-list ray scan (RL_WL, the streaming kernel's jittered C5 rays).  ring_rays visits every
-// block that SOME lane's ray line may cross (the wave union) and tests its entries for all of
-// the wave's samples; on C5 (seeded alpha: normals in every direction) that union is ~100 % of
-// the blocks while one ray line needs ~33 % of them.  Here each lane's samples test only
-// their own blocks:
-//   1. per sample, the block circle tests of ring_rays (the same fp32 expressions) give a
-//      mask of the blocks its ray line may cross;
-//   2. the wave compacts the (sample slot, block) pairs into an LDS list (prefix sums);
-//   3. rounds of 64*CK items: each lane takes CK consecutive items, loads each item's sample
-//      (P, n) from the kernel's arrays, evaluates the 16 entries' side bits of the item's
-//      block exactly as ring_rays does (fp32, CK items packed), walks the candidates with the
-//      exact reference test, and folds its minima into the sample's LDS slots with 64-bit
-//      atomic minima (bp, bn and ub2 are >= +0 or +inf, so their bit patterns order like the
-//      values; NaN patterns sort above +inf, as fmin / the `t < best` tests ignore NaNs).
-// Per sample the candidate set is the one ring_rays walks (a block the sample's own circle
-// test rejects yields no candidate in ring_rays either), and the minima do not depend on the
-// order of the candidates, so bp, bn and ub2 are ring_rays' bit for bit.
-template <int CK>
-struct WlScratch {
-    static constexpr int CAP = 64 * CK * 4;   // items per list window (4 rounds)
-    unsigned long long res[3][64 * CK];      // per sample slot: bp, bn, ub2 bit patterns
-    uint16_t item[CAP];                      // (slot << 5) | block within the group of 32
-};
-// where the wave's samples live: slot s = lane*CK + k is sample `base + s` of x, y, nx, ny
-struct WlSamples {
-    const double* x;
-    const double* y;
-    const double* nx;
-    const double* ny;
-    int base;
-};
-__device__ __forceinline__ void wl_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-template <int CK>
-__device__ __forceinline__ void ring_rays_wl(const RingDesc& R, const double (&qx)[CK], const double (&qy)[CK],
-                                             const double (&ux)[CK], const double (&uy)[CK], const bool (&act)[CK],
-                                             double (&bp)[CK], double (&bn)[CK], double (&ub2)[CK],
-                                             const WlSamples& smp, WlScratch<CK>& ws) {
-    const float* __restrict__ V = (const float*)(R.blk + ring_blk_off_vtx32(R.M));   // per-lane reads
-    cflt* BK = (cflt*)(R.blk + ring_blk_off_blk32(R.M));                              // uniform reads
-    const uint32_t* __restrict__ F = R.flag;
-    const SegRec* __restrict__ S = R.rec;
-    const int lane = threadIdx.x & 63;
-    constexpr unsigned long long INFB = 0x7ff0000000000000ull;
-    // the fp32 ray constants of a sample, as ring_rays computes them
-    auto consts = [&](double px, double py, double nxv, double nyv, float& g, float& dl, float& ufx, float& ufy,
-                      bool& bad) {
-        const double q1 = fabs(px) + fabs(py);
-        g = (float)(nxv * py - nyv * px);
-        dl = (float)((R.dl0 + 4e-15 * q1) + (R.dl32 + 1e-6 * q1));
-        ufx = (float)nxv;
-        ufy = (float)nyv;
-        bad = !(isfinite(g) && isfinite(dl) && isfinite(ufx) && isfinite(ufy));
-    };
-    float g[CK], dl[CK], uxf[CK], uyf[CK];
-    bool badk[CK];
-#pragma unroll
-    for (int k = 0; k < CK; ++k) {
-        consts(qx[k], qy[k], ux[k], uy[k], g[k], dl[k], uxf[k], uyf[k], badk[k]);
-        ws.res[0][lane * CK + k] = INFB;
-        ws.res[1][lane * CK + k] = INFB;
-        ws.res[2][lane * CK + k] = INFB;
-    }
-    const int nb = R.M / RL_BLK;
-    for (int g0 = 0; g0 < nb; g0 += 32) {
-        const int ng = nb - g0 < 32 ? nb - g0 : 32;
-        // 1. per-sample block masks (the block test of ring_rays, per sample)
-        uint32_t mask[CK];
-#pragma unroll
-        for (int k = 0; k < CK; ++k) mask[k] = 0u;
-        for (int q = 0; q < ng; ++q) {
-            cflt* bk = BK + 4 * (g0 + q);
-            const float cx = bk[0], cy = bk[1], rb = bk[2];
-            if (rb >= 0.0f) {
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    const float c = __builtin_fmaf(uxf[k], cy, -__builtin_fmaf(uyf[k], cx, g[k]));
-                    if (act[k] && !(fabsf(c) > rb * (1.0f + 1e-6f) + 2.0f * dl[k])) mask[k] |= 1u << q;
-                }
-            }
-        }
-        // 2. exclusive prefix of the item counts over the wave (lane order, then k)
-        int cnt = 0;
-#pragma unroll
-        for (int k = 0; k < CK; ++k) cnt += __popc(mask[k]);
-        int incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += o;
-        }
-        const int off = incl - cnt;
-        const int total = __shfl(incl, 63, 64);
-        if (threadIdx.x % 64 == 0) { RL_CNT(0, 4); RL_CNT(1, (total + 63) / 64); }
-        for (int w = 0; w < total; w += WlScratch<CK>::CAP) {
-            // items with list index in [w, w + CAP)
-            int idx = off;
-#pragma unroll
-            for (int k = 0; k < CK; ++k) {
-                uint32_t m = mask[k];
-                while (m) {
-                    const int bq = __ffs(m) - 1;
-                    m &= m - 1u;
-                    if (idx >= w && idx < w + WlScratch<CK>::CAP)
-                        ws.item[idx - w] = (uint16_t)(((lane * CK + k) << 5) | bq);
-                    ++idx;
-                }
-            }
-            wl_fence();
-            const int nw = total - w < WlScratch<CK>::CAP ? total - w : WlScratch<CK>::CAP;
-            for (int r0 = 0; r0 < nw; r0 += 64 * CK) {
-                // 3. this lane's CK items
-                int slot[CK], e0[CK];
-                bool has[CK];
-                double px[CK], py[CK], pnx[CK], pny[CK];
-                float gi[CK], dli[CK], fx[CK], fy[CK];
-                bool badi[CK];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    const int i = r0 + lane * CK + k;
-                    has[k] = i < nw;
-                    const int it = has[k] ? (int)ws.item[i] : 0;
-                    slot[k] = it >> 5;
-                    e0[k] = (g0 + (it & 31)) * RL_BLK;
-                    const int si = smp.base + slot[k];
-                    px[k] = smp.x[si]; py[k] = smp.y[si]; pnx[k] = smp.nx[si]; pny[k] = smp.ny[si];
-                    consts(px[k], py[k], pnx[k], pny[k], gi[k], dli[k], fx[k], fy[k], badi[k]);
-                }
-                auto side = [&](int k, float vx, float vy) -> float { return __builtin_fmaf(fx[k], vy, -__builtin_fmaf(fy[k], vx, gi[k])); };
-                auto sgn = [](float x) -> uint32_t { return __float_as_uint(x) >> 31; };
-                uint32_t cand[CK];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    // bit 16: the entry before the block, bit 15-j: entry e0+j (ring_rays' order)
-                    uint32_t pb = 0u, qb = 0u;
-                    if (e0[k] > 0) {
-                        const float c = side(k, V[2 * (e0[k] - 1)], V[2 * (e0[k] - 1) + 1]);
-                        pb = sgn(dli[k] - c);
-                        qb = sgn(c + dli[k]);
-                    }
-#pragma unroll
-                    for (int j = 0; j < RL_BLK; ++j) {
-                        const float c = side(k, V[2 * (e0[k] + j)], V[2 * (e0[k] + j) + 1]);
-                        pb = __builtin_amdgcn_alignbit(pb, __float_as_uint(dli[k] - c), 31);
-                        qb = __builtin_amdgcn_alignbit(qb, __float_as_uint(c + dli[k]), 31);
-                    }
-                    constexpr uint32_t BM = RL_BLK >= 32 ? 0xffffffffu : ((1u << RL_BLK) - 1u);
-                    uint32_t cd = ~((pb & (pb >> 1)) | (qb & (qb >> 1))) & BM;
-                    if (badi[k]) cd = BM;
-                    // segment flags of the block's entries (bit 31-(e%32) of word e/32)
-                    const uint32_t fw = F[e0[k] >> 5] << (e0[k] & 31);
-                    cd &= fw >> (32 - RL_BLK);
-                    cand[k] = has[k] ? cd : 0u;
-                }
-                // exact tests of each item's candidates
-                double lbp[CK], lbn[CK], lub[CK];
-#pragma unroll
-                for (int k = 0; k < CK; ++k) lbp[k] = lbn[k] = lub[k] = INFINITY;
-                for (;;) {
-                    bool any = false, h[CK];
-                    int j[CK];
-#pragma unroll
-                    for (int k = 0; k < CK; ++k) {
-                        h[k] = cand[k] != 0u;
-                        j[k] = h[k] ? __clz(cand[k]) - (32 - RL_BLK) : 0;
-                        cand[k] &= ~((1u << (RL_BLK - 1)) >> j[k]);
-                        any |= h[k];
-                    }
-                    if (!__any(any)) break;
-                    double x0[CK], y0[CK], sx[CK], sy[CK];
-#pragma unroll
-                    for (int k = 0; k < CK; ++k) {
-                        const SegRec* sr = S + e0[k] + j[k];
-                        x0[k] = sr->x0; y0[k] = sr->y0; sx[k] = sr->vx; sy[k] = sr->vy;
-                    }
-#pragma unroll
-                    for (int k = 0; k < CK; ++k) {
-                        if (h[k]) {
-                            RL_CNT(3, 1);
-                            ray_exact(x0[k], y0[k], sx[k], sy[k], px[k], py[k], pnx[k], pny[k], lbp[k], lbn[k]);
-                            const double ax = px[k] - x0[k], ay = py[k] - y0[k];
-                            const double ex = ax - sx[k], ey = ay - sy[k];
-                            lub[k] = fmin(lub[k], fmin(ax * ax + ay * ay, ex * ex + ey * ey));
-                        }
-                    }
-                    if (threadIdx.x % 64 == 0) RL_CNT(2, 1);
-                }
-#pragma unroll
-                for (int k = 0; k < CK; ++k) {
-                    if (has[k]) {
-                        if (lbp[k] < INFINITY) atomicMin(&ws.res[0][slot[k]], (unsigned long long)__double_as_longlong(lbp[k]));
-                        if (lbn[k] < INFINITY) atomicMin(&ws.res[1][slot[k]], (unsigned long long)__double_as_longlong(lbn[k]));
-                        if (lub[k] < INFINITY) atomicMin(&ws.res[2][slot[k]], (unsigned long long)__double_as_longlong(lub[k]));
-                    }
-                }
-            }
-            wl_fence();
-        }
-    }
-    wl_fence();
-#pragma unroll
-    for (int k = 0; k < CK; ++k) {
-        bp[k] = __longlong_as_double((long long)ws.res[0][lane * CK + k]);
-        bn[k] = __longlong_as_double((long long)ws.res[1][lane * CK + k]);
-        ub2[k] = __longlong_as_double((long long)ws.res[2][lane * CK + k]);
-    }
-    wl_fence();
-}
+// (A work-list form of the ray scan -- each lane's samples testing only their own blocks
+// from a compacted (sample, block) list in LDS, per-lane vertex loads and LDS atomic minima --
+// was built in round 5 and measured 40 % slower on C5: DESIGN.md §3f.)
 
 // minDistanceToSegments_global (ref:501-512) for the samples with need[k], exact for
 // every sample whose minimum is <= rad[k] (md[k] = +inf or a value > rad[k] otherwise).
@@ -710,19 +502,5 @@ __device__ __forceinline__ void corridor_bounds(const RingDesc& Ri, const RingDe
     corridor_finish<CK, TIGHT, PRUNE>(Ri, Ro, qx, qy, act, guard, bp, bn, ub2, lo, hi, stamp);
 }
 
-// corridor_bounds with the work-list ray scan (ring_rays_wl; same results bit for bit)
-template <int CK, bool TIGHT = true, bool PRUNE = true, class Stamp = NoStamp>
-__device__ __forceinline__ void corridor_bounds_wl(const RingDesc& Ri, const RingDesc& Ro, const double (&qx)[CK],
-                                                   const double (&qy)[CK], const double (&ux)[CK],
-                                                   const double (&uy)[CK], const bool (&act)[CK], double guard,
-                                                   double (&lo)[CK], double (&hi)[CK], const WlSamples& smp,
-                                                   WlScratch<CK>& ws, Stamp stamp = Stamp()) {
-    double bp[2][CK], bn[2][CK], ub2[2][CK];
-    ring_rays_wl<CK>(Ri, qx, qy, ux, uy, act, bp[0], bn[0], ub2[0], smp, ws);
-    stamp(8);
-    ring_rays_wl<CK>(Ro, qx, qy, ux, uy, act, bp[1], bn[1], ub2[1], smp, ws);
-    stamp(9);
-    corridor_finish<CK, TIGHT, PRUNE>(Ri, Ro, qx, qy, act, guard, bp, bn, ub2, lo, hi, stamp);
-}
 
 }  // namespace rl

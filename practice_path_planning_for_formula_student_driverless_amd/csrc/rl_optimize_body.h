@@ -541,6 +541,35 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             if (k < cnt) { NX[i] = ox; NY[i] = oy; }
         }
     };
+    // normals (as `normals`) and the curvature of heading_curv_from_points_generic
+    // (ref:595-620) from one load of the path: the min-time latency shapes (VSPLIT) need the
+    // curvature before the v-pass wave starts, and computing it beside the normals takes it
+    // off the path to the split
+    auto normals_kappa = [&](double (&kaout)[K]) RL_AI {
+        double px[K + 4], py[K + 4];
+        loadP(px, py);
+        const int bs = opaque(base);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = bs + k;
+            double tx, ty;
+            if (N == 1) { tx = 1; ty = 0; }
+            else if (CLOSED) { tx = (px[k + 3] - px[k + 1]) * 0.5; ty = (py[k + 3] - py[k + 1]) * 0.5; }
+            else if (i == 0) { tx = px[k + 3] - px[k + 2]; ty = py[k + 3] - py[k + 2]; }
+            else if (i == N - 1) { tx = px[k + 2] - px[k + 1]; ty = py[k + 2] - py[k + 1]; }
+            else { tx = (px[k + 3] - px[k + 1]) * 0.5; ty = (py[k + 3] - py[k + 1]) * 0.5; }
+            if (sqrt(tx * tx + ty * ty) < 1e-15) { tx = 1; ty = 0; }
+            double vx = -ty, vy = tx;
+            double n = sqrt(vx * vx + vy * vy);              // geom::normalize ref:132
+            double ox = 0, oy = 0;
+            if (!(n < 1e-15)) { ox = vx / n; oy = vy / n; }
+            if (active && k < cnt) { NX[i] = ox; NY[i] = oy; }
+            double xp, yp, xpp, ypp;
+            deriv(px, py, k, xp, yp, xpp, ypp);
+            const double kav = (xp * ypp - yp * xpp) / pow15(smax(1e-12, xp * xp + yp * yp));
+            kaout[k] = (active && k < cnt) ? kav : 0.0;
+        }
+    };
     // corridor blocks ref:701-711 / 749-756 (guard = width*0.5 + margin). The scan runs
     // in its own mapping: pass c gives lane t the CKK adjacent samples from (c*T+t)*CKK,
     // so a wave holds 64*CKK consecutive samples whose rays are spatially coherent and
@@ -1272,11 +1301,19 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             }
         };
         const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
+        double ka[K];
+        bool ka_done = false;                                    // (uniform)
         if (outer < MO) {
             // normals + corridor (ref:692-711 initially with the veh_width argument,
             // ref:746-756 after each update with cfg veh_width_m)
             if (tid == 0) sm.ctr = 0;                            // read after the barrier below
-            normals();
+            if constexpr (VSPLIT) {
+                normals_kappa(ka);
+                vsv[tid] = ka[0];
+                ka_done = true;
+            } else {
+                normals();
+            }
             __syncthreads();
             if constexpr (!VSPLIT) {                             // (VSPLIT: beside the v-pass below)
                 corridor(guard, lo, hi);
@@ -1284,8 +1321,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             }
         }
         RL_STAMP(1);
-        double ka[K];
-        if (MT || outer == MO) {
+        if ((MT || outer == MO) && !ka_done) {
             // heading_curv_from_points_generic ref:595-620
             double hd[K];
             double px[K + 4], py[K + 4];
@@ -1312,13 +1348,25 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             if constexpr (VSPLIT) {
                 // the v-pass on the last wave, the corridor on the others, then both results
                 // reach their owners through LDS
-                vsv[tid] = ka[0];
-                __syncthreads();
+                if (!ka_done) {                                  // (the final outer iteration)
+                    vsv[tid] = ka[0];
+                    __syncthreads();
+                }
+                RL_STAMP(2);                                     // (stamps: curvature)
                 if (wid_u == NW - 1) {
                     const int sw = vpass1w();                    // ref:947 / 1047
                     if (lane == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
+#if defined(RL_STAMPS) && !defined(RL_STAMPS_EVAL)
+                    RL_STAMP(12);                                // (the v-pass wave's own slot)
+#endif
                 } else if (outer < MO) {
+#if defined(RL_STAMPS) && !defined(RL_STAMPS_EVAL)
+                    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
                     corridor_scan(guard);
+                    if (wid_u < 3) st_acc[13 + wid_u] += __builtin_amdgcn_s_memtime() - ts0;   // per-wave scan time
+#else
+                    corridor_scan(guard);
+#endif
                 }
                 if (outer < MO) {
                     corridor_collect(lo, hi);                    // (its first barrier joins the two)
@@ -1326,6 +1374,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 } else {
                     __syncthreads();
                 }
+#if defined(RL_STAMPS) && !defined(RL_STAMPS_EVAL)
+                RL_STAMP(11);                                    // (wave 0: the join's wait + collect)
+#endif
                 v[0] = active ? vsv[tid] : INFINITY;
             } else {
                 const int sw = vpass(ka, v);                     // ref:947 / 1047
@@ -1549,7 +1600,12 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #ifdef RL_STAMPS
     RL_STAMP(6);
     if (tid == 0 && b < 16384) {
-        for (int i = 0; i < 16; ++i) rl_dbg_stamps[b][i] = st_acc[i];
+        for (int i = 0; i < 16; ++i)
+            if (!(VSPLIT && (i == 12 || i == 14 || i == 15))) rl_dbg_stamps[b][i] = st_acc[i];
+    }
+    if (VSPLIT && lane == 0 && b < 16384) {                  // the v-pass wave; waves 1, 2's scans
+        if (wid == NW - 1) rl_dbg_stamps[b][12] = st_acc[12];
+        else if (wid == 1 || wid == 2) rl_dbg_stamps[b][13 + wid] = st_acc[13 + wid];
     }
 #endif
 }

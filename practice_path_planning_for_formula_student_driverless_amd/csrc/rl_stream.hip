@@ -95,16 +95,10 @@ __device__ __forceinline__ double wave_sum_s(double x) {
 #endif
 constexpr int RED_SLOTS = 3 * RL_BT_BATCH > 4 ? 3 * RL_BT_BATCH : 4;
 
-// corridor ray scans: the work-list form of rl_corridor.h (each lane's samples test only
-// their own blocks), RL_SWL = 0 keeps the wave-union scan (A/B knob)
-#ifndef RL_SWL
-#define RL_SWL 0
-#endif
 struct SSmem {
     double red[RED_SLOTS][NWS];
-    union {
-        double vin[2][TS];             // v-pass relaxation (the corridor phase is over by then)
-        WlScratch<RL_SCK> wl[NWS];     // corridor work lists, one per wave
+    struct {
+        double vin[2][TS];             // v-pass relaxation
     } u;
     // warm start of the v-pass relaxations: per thread, the incoming value its chunk ended
     // with in [0] the first forward sweep of the previous v pass, [1] the latest forward
@@ -169,6 +163,8 @@ __global__ __launch_bounds__(TS, RL_STS_MINW) void rl_stream_kernel(KParams p, S
 __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb) {
 #endif
     __shared__ SSmem sm;
+    // the register-resident v-pass's curvatures (RL_SVP_MAX samples per thread; vpass_reg)
+    __shared__ double ska[MT && RL_SVP_REG ? RL_SVP_MAX * TS + RL_SVP_MAX : 1];
 #ifdef RL_STAMPS
     unsigned long long st_acc[16] = {};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
@@ -423,12 +419,16 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         constexpr int CR = decltype(crc)::value;
         const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
         const int cnt = r1 - r0;                  // CR, except the last active thread; 0 beyond N
-        double ka[CR], v[CR];
+        // the chunk's curvatures stay in LDS (read-only for the whole v pass; each thread
+        // reads only its own entries, so no barrier): in registers they spilled to scratch
+        // (the 128-VGPR budget of 1024 threads), reloaded inside every step
+        double* const ka = &ska[r0];
+        double v[CR];
 #pragma unroll
         for (int k = 0; k < CR; ++k) {
-            ka[k] = 0.0;
-            if (k < cnt) ka[k] = KA[r0 + k];
-            const double kk = fabs(ka[k]);
+            const double kv = (k < cnt) ? KA[r0 + k] : 0.0;
+            ka[k] = kv;                           // (the padding slots past N hold 0)
+            const double kk = fabs(kv);
             const double vk = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
             v[k] = (k < cnt) ? vk : INFINITY;
         }
@@ -621,24 +621,12 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                     act[k] = i0 + k < N;
                 }
-#if RL_SWL
-                const WlSamples smp{X, Y, NX, NY, c * 64 * RL_SCK};
-#endif
 #ifdef RL_STAMPS
                 RL_SSTAMP(7);
-#if RL_SWL
-                corridor_bounds_wl<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk, smp, sm.u.wl[wid],
-                                           [&](int s) { RL_SSTAMP(s); });
-#else
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk,
                                         [&](int s) { RL_SSTAMP(s); });
-#endif
-#else
-#if RL_SWL
-                corridor_bounds_wl<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk, smp, sm.u.wl[wid]);
 #else
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
-#endif
 #endif
 #pragma unroll
                 for (int k = 0; k < RL_SCK; ++k) {

@@ -13,6 +13,10 @@ lib = abi.load_library(os.path.join(REPO, f"practice_path_planning_for_formula_s
 names = ["setup", "corridor tail", "mt:κ/vpass/γ", "lin-geom", "PGD loop (rest)", "update", "final",
          "normals + corridor loads", "corridor: inner rays", "corridor: outer rays", "corridor: fallback",
          "pgd: projection", "pgd: stencil+partials", "pgd: wave sum", "pgd: barrier+block sum", "pgd: gradient"]
+if VAR == "stamps":     # VSPLIT (min-time, K = 1): slot 11 = wave 0's join wait + collect, 12 = the v-pass wave
+    names[11], names[12] = "vsplit: join wait + collect (wave 0)", "vsplit: v-pass wave's v-pass [not in the sum]"
+    names[13], names[14], names[15] = ("vsplit: wave 0 scan [in 7-10]", "vsplit: wave 1 scan [not in the sum]",
+                                       "vsplit: wave 2 scan [not in the sum]")
 for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n2000"):
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)
     for mode in (1, 2):
@@ -29,8 +33,9 @@ for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n20
                  lib.rl_debug_stamps_lat if not thr else lib.rl_debug_stamps)
             assert f(st.ctypes.data_as(C.c_void_p), 1) == 0
             tot = st.sum(0).astype(float)
+            w0 = tot.sum() - (tot[12:16].sum() if VAR == "stamps" else 0.0)   # wave 0's own cycles
             print(f"{cname} N={prob.N} mode={mode} shape=({K},{T}) kernel {ms.value:.3f} ms (stamped); "
-                  f"wave-0 cycles {tot.sum():.3e}: " +
-                  ", ".join(f"{nm} {100 * tot[i] / tot.sum():.1f}%" for i, nm in enumerate(names) if tot[i] > 0), flush=True)
+                  f"wave-0 cycles {w0:.3e}: " +
+                  ", ".join(f"{nm} {100 * tot[i] / w0:.1f}%" for i, nm in enumerate(names) if tot[i] > 0), flush=True)
             lib.rl_plan_destroy(h)
 os.environ.pop("RL_LAT_SHAPES", None)
