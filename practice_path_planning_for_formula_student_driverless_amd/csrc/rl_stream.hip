@@ -303,6 +303,23 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         return acc;
     };
 
+    // time weight gamma^2 of one sample (ref:950-977) from its curvature and speed
+    auto gamma2_of = [&](double kap, double vv, double v_avg) -> double {
+        double vkappa = sqrt(C.a_lat_max / smax(fabs(kap), C.kappa_eps));
+        double rr = smin(1.0, vv / smax(1e-6, vkappa));
+        double r = smin(1.0, smax(0.0, rr * rr));
+        double rp = (C.time_gamma_power == 2.0) ? r * r : pow_stream(r, C.time_gamma_power);
+        double corner_w = 1.0 + C.w_time_gain * rp;
+        double invv_w = 1.0;
+        if (C.time_weight_use_inv_v) {
+            double ratio = v_avg / smax(1e-6, vv);
+            invv_w = 1.0 + C.inv_v_gain * (ratio - 1.0);
+            if (invv_w < 1.0) invv_w = 1.0;
+            if (invv_w > 3.0) invv_w = 3.0;
+        }
+        double gamma = corner_w * invv_w;
+        return gamma * gamma;
+    };
     // ---- v(s) profile (ref:782-862), contiguous ranges [t*Cr, t*Cr+Cr) --------
     if (tid == 0) {
         VConst vc;
@@ -415,7 +432,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     // value included).  Rounds end when no published value changes.  Padding slots of the
     // partial last chunk hold ka = 0, v = +inf and never bind.  Same fixed point, bit for bit.
     auto same_bits = [](double a, double b) -> bool { return __double_as_longlong(a) == __double_as_longlong(b); };
-    auto vpass_reg = [&](auto crc) -> int {
+    // g2: also finish the outer iteration's time weights from the registers (gamma^2 needs no
+    // block-wide value unless time_weight_use_inv_v, which the caller excludes): G2 is written
+    // directly and V, which only the weights would read, is not
+    auto vpass_reg = [&](auto crc, bool g2) -> int {
         constexpr int CR = decltype(crc)::value;
         const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
         const int cnt = r1 - r0;                  // CR, except the last active thread; 0 beyond N
@@ -552,15 +572,23 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             RL_SSTAMP(14);
         }
         RL_SSTAMP(14);
+        if (g2) {
 #pragma unroll
-        for (int k = 0; k < CR; ++k)
-            if (k < cnt) V[r0 + k] = v[k];
+            for (int k = 0; k < CR; ++k)
+                if (k < cnt) G2[r0 + k] = gamma2_of(ka[k], v[k], 0.0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < CR; ++k)
+                if (k < cnt) V[r0 + k] = v[k];
+        }
         return sweeps;
     };
-    auto vpass_any = [&]() -> int {
+    // g2_done: the register path wrote G2 itself (requested by g2)
+    auto vpass_any = [&](bool g2, bool& g2_done) -> int {
+        g2_done = false;
         if (RL_SVP_REG) {
             switch (Cr) {
-#define RL_SVP_CASE(n) case n: if (n >= RL_SVP_MIN && n <= RL_SVP_MAX) return vpass_reg(std::integral_constant<int, n>()); break;
+#define RL_SVP_CASE(n) case n: if (n >= RL_SVP_MIN && n <= RL_SVP_MAX) { g2_done = g2; return vpass_reg(std::integral_constant<int, n>(), g2); } break;
                 RL_SVP_CASE(5) RL_SVP_CASE(6) RL_SVP_CASE(7) RL_SVP_CASE(8)
                 RL_SVP_CASE(9) RL_SVP_CASE(10) RL_SVP_CASE(11) RL_SVP_CASE(12)
 #undef RL_SVP_CASE
@@ -661,7 +689,8 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             __syncthreads();
         }
         if (MT) {
-            const int sw = vpass_any();                            // ref:947 / 1047
+            bool g2_done;
+            const int sw = vpass_any(outer < MO && !C.time_weight_use_inv_v, g2_done);   // ref:947 / 1047
             RL_SSTAMP(11);
             if (tid == 0 && p.sweeps) p.sweeps[(size_t)b * (MO + 1) + outer] = sw;
             __syncthreads();
@@ -676,7 +705,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 }
                 block_sum_s<1>(sm, lt, lane, wid);
                 if (tid == 0 && p.lap) p.lap[b] = lt[0];
-            } else {
+            } else if (!g2_done) {
                 double v_avg = 0.0;
                 if (C.time_weight_use_inv_v) {
                     double vs[1] = {0.0};
@@ -684,22 +713,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     block_sum_s<1>(sm, vs, lane, wid);
                     v_avg = vs[0] / (double)(N > 1 ? N : 1);
                 }
-                for (int i = tid; i < N; i += TS) {                // ref:950-977
-                    double vkappa = sqrt(C.a_lat_max / smax(fabs(KA[i]), C.kappa_eps));
-                    double rr = smin(1.0, V[i] / smax(1e-6, vkappa));
-                    double r = smin(1.0, smax(0.0, rr * rr));
-                    double rp = (C.time_gamma_power == 2.0) ? r * r : pow_stream(r, C.time_gamma_power);
-                    double corner_w = 1.0 + C.w_time_gain * rp;
-                    double invv_w = 1.0;
-                    if (C.time_weight_use_inv_v) {
-                        double ratio = v_avg / smax(1e-6, V[i]);
-                        invv_w = 1.0 + C.inv_v_gain * (ratio - 1.0);
-                        if (invv_w < 1.0) invv_w = 1.0;
-                        if (invv_w > 3.0) invv_w = 3.0;
-                    }
-                    double gamma = corner_w * invv_w;
-                    G2[i] = gamma * gamma;
-                }
+                for (int i = tid; i < N; i += TS) G2[i] = gamma2_of(KA[i], V[i], v_avg);   // ref:950-977
             }
         }
         RL_SSTAMP(2);
