@@ -455,6 +455,11 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #define RL_GHOST_KMAX 2      // ghost samples for K <= this (A/B knob)
 #endif
     constexpr bool GHOST = RL_GHOST && NW > 1 && K <= RL_GHOST_KMAX;
+    // min-time latency shapes: the v-pass on one wave beside the corridor (VSPLIT, see vpass1w)
+#ifndef RL_VSPLIT
+#define RL_VSPLIT 1
+#endif
+    constexpr bool VSPLIT = RL_VSPLIT && MT && K == 1 && NW >= 2 && T <= 512;
     // Speculative gradient (latency shapes): every trial's gradient is evaluated before its
     // Armijo test (the bundled tracks accept 120 of 122-137 trials per outer iteration), so
     // the gradient's LDS reads and arithmetic run beside the J/decrease sums instead of
@@ -836,10 +841,6 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // consecutive samples per lane and relaxes them within the wave (DPP only, no barrier),
     // with the warm start and early stops of `vpass`; curvature in and speeds out go through
     // LDS (vsv).  Same fixed point, so the same values bit for bit.
-#ifndef RL_VSPLIT
-#define RL_VSPLIT 1
-#endif
-    constexpr bool VSPLIT = RL_VSPLIT && MT && K == 1 && NW >= 2 && T <= 512;
     constexpr int KP = VSPLIT ? T / 64 : 1;
     __shared__ double vsv[VSPLIT ? T : 1];
     double vwg[4] = {INFINITY, INFINITY, INFINITY, INFINITY};   // warm starts (the v-pass wave's lanes)
@@ -1359,6 +1360,11 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #if defined(RL_STAMPS) && !defined(RL_STAMPS_EVAL)
                     RL_STAMP(12);                                // (the v-pass wave's own slot)
 #endif
+                    // then the corridor chunks still in the queue: the 64-sample chunks of a
+                    // bundled track (N = 187-261: 3-5 chunks) fall unevenly on the other waves
+                    // (phase stamps: the join waited for the wave with two; two samples per lane
+                    // instead, 128-sample chunks, was slower: training_map 1.49 -> 1.56 ms)
+                    if (outer < MO) corridor_scan(guard);
                 } else if (outer < MO) {
 #if defined(RL_STAMPS) && !defined(RL_STAMPS_EVAL)
                     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
