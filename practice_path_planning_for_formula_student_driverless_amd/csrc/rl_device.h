@@ -48,13 +48,15 @@ static_assert(sizeof(SegRec) == 64, "SegRec must be 64 B");
 
 // Derived v-pass constants, evaluated exactly as the reference expressions
 // of ax_max_at (ref:797-824) evaluate their constant prefixes.
+// 72 bytes: it sits in every kernel's LDS block, whose size is allocated in 512-byte granules
+// (one field more put the (4, 64) / (8, 64) blocks one granule over: C4 concurrent wall
+// +30% at equal kernel times, profiles/r05/ab_c4_lds.log)
 struct VConst {
-    double a_total;     // use_total_ge_lat ? max(a_total_max, a_lat_max) : a_total_max
-    double a_total2;    // a_total*a_total
+    double a_total2;    // a_total^2, a_total = use_total_ge_lat ? max(a_total_max, a_lat_max) : a_total_max
     double kFd;         // (0.5*rho_air)*Cd*A_front_m2
     double Fr;          // mass_kg*9.81*c_rr
     double mass, Pmax, acc_cap, brk_cap;
-    double h, two_h;
+    double h;
     int32_t pw_free;    // the power limit can never bind (see power_never_binds); read per step
     int32_t _pad;
 };
@@ -66,9 +68,9 @@ struct VConst {
 // of the LDS table: the register-resident relaxations hold 3 x Cr doubles per lane already
 __device__ __forceinline__ VConst vconst_uniform(const VConst& s) {
     VConst c;
-    c.a_total = uni(s.a_total); c.a_total2 = uni(s.a_total2); c.kFd = uni(s.kFd); c.Fr = uni(s.Fr);
+    c.a_total2 = uni(s.a_total2); c.kFd = uni(s.kFd); c.Fr = uni(s.Fr);
     c.mass = uni(s.mass); c.Pmax = uni(s.Pmax); c.acc_cap = uni(s.acc_cap); c.brk_cap = uni(s.brk_cap);
-    c.h = uni(s.h); c.two_h = uni(s.two_h);
+    c.h = uni(s.h);
     c.pw_free = __builtin_amdgcn_readfirstlane(s.pw_free);
     c._pad = 0;
     return c;
@@ -86,6 +88,9 @@ __device__ __forceinline__ VConst vconst_uniform(const VConst& s) {
 // min(a_res, acc_cap) bit for bit.
 __device__ __forceinline__ bool power_never_binds(double Pmax, double mass, double kFd, double Fr, double v_cap,
                                                   double acc_cap) {
+#if defined(RL_PWF) && RL_PWF == 0
+    return false;                    // A/B knob: always evaluate the power limit
+#endif
     if (!(Pmax > 0.0) || !(mass > 0.0) || !(v_cap > 1e-6) || !(kFd >= 0.0) || !(Fr >= 0.0)) return false;
     if (!(Pmax < 1e300) || !(mass < 1e300) || !(v_cap < 1e150) || !(kFd < 1e300) || !(Fr < 1e300)) return false;
     if (!(acc_cap < 1e8) || !(acc_cap > -1e300)) return false;
@@ -145,7 +150,11 @@ __device__ __forceinline__ double vstep_fwd(const VConst& c, double vi, double k
     double alat = vi * vi * fabs(ki);
     double a_res = sqrt(vs_max0(c.a_total2 - alat * alat));
     double a_acc = vs_min(a_res, c.acc_cap);
-    if (!__builtin_amdgcn_readfirstlane(c.pw_free)) {   // uniform per instance (power_never_binds)
+#if defined(RL_PW_BRANCH) && RL_PW_BRANCH == 0
+    if (true) {
+#else
+    if (!__builtin_amdgcn_readfirstlane(c.pw_free)) {
+#endif   // uniform per instance (power_never_binds)
         double Fd = c.kFd * vi * vi;
 #if RL_VSTEP_FAST
         // evaluated unconditionally and selected: as the arm of a branch its two divisions ran

@@ -219,29 +219,58 @@ __device__ __forceinline__ void put(double (&a)[K], int idx, double v) {
     }
 }
 
-template <int K, int T, bool MT>
-struct alignas(16) Smem {
-    static constexpr int NW = T / 64;
-    // The small tables come first: their (mostly wave-uniform) addresses then fit the
-    // 16-bit offset field of ds_read/ds_write, so one base register serves them all.
-    //
-    // Edge tables of the neighbour exchange, one row per exchange slot.  Every lane
-    // stores (branch-free): the lane that publishes into its row's tail, every other lane
-    // into its own entry of the row's head (a sink nobody reads).  One address register
-    // per table serves all four slots (the slot is an immediate offset).
+// v-pass warm starts (min-time, see vpass): 0 off, 1 multi-wave shapes only, 2 every
+// min-time shape.  In the one-wave (K, 64) throughput shapes (C1/C4) the in-wave rounds are
+// cheap DPP steps and the starts leave the kernel time as it is, while their 2 KB table
+// costs LDS granules that concurrent plans share (C4 min-time 8.7 -> 11.9 ms wall at equal
+// kernel times, scripts/ab_c4_single.py, profiles/r05/ab_c4_lds.log)
+#ifndef RL_WARM
+#define RL_WARM 1
+#endif
+template <int T, bool MT>
+struct WarmStart {
+    static constexpr bool value = MT && (RL_WARM == 2 || (RL_WARM == 1 && T > 64));
+};
+
+// min-time: warm start of the v-pass relaxations, per thread the incoming value its chunk
+// ended with in [0] the first forward sweep of the previous v pass, [1] the latest forward
+// sweep, [2] / [3] the same for the backward sweeps (+inf: none yet; see vpass).  An empty
+// base (no bytes) in the shapes without warm starts.
+template <int T, bool WARM>
+struct WarmTab {
+    double vg[4][T];
+};
+template <int T>
+struct WarmTab<T, false> {};
+
+// Edge tables of the neighbour exchange, one row per exchange slot.  Every lane stores
+// (branch-free): the lane that publishes into its row's tail, every other lane into its own
+// entry of the row's head (a sink nobody reads).  One address register per table serves
+// all four slots (the slot is an immediate offset).  One wave exchanges by readlane and
+// needs none: an empty base, 6 KB less LDS per (K, 64) block.
+template <int NW>
+struct PubTab {
     static constexpr int RF = 64 + NW;
     double pubF[4][RF];          // [s][64 + w]: first value of lane 0 of wave w
     double pubL[4][RF];          // [s][64 + w]: last value of lane 63 of wave w
     double pubW[4][65];          // [s][64]: last valid value of the last active thread (closed wrap)
+};
+template <>
+struct PubTab<1> {};
+
+// The small tables come first: their (mostly wave-uniform) addresses then fit the 16-bit
+// offset field of ds_read/ds_write, so one base register serves them all.  The block size
+// is allocated in 512-byte LDS granules and sets how many blocks of concurrent plans share
+// a CU: one granule more on the (4, 64) / (8, 64) min-time blocks cost the C4 concurrent
+// sweep 30% at equal kernel times (profiles/r05/ab_c4_lds.log).
+template <int K, int T, bool WARM>
+struct alignas(16) Smem : PubTab<T / 64>, WarmTab<T, WARM> {
+    static constexpr int NW = T / 64;
     double red[3][NW];           // per-wave partial sums of an evaluation
     double red2[2][NW];          // other block reductions
     double bc[4];                // broadcast scalars
     int ctr;                     // corridor work queue: next chunk of 64*CK samples
     VConst vc;                   // v-pass constants (read per v pass: no registers held across the kernel)
-    // min-time: warm start of the v-pass relaxations, per thread the incoming value its chunk
-    // ended with in [0] the first forward sweep of the previous v pass, [1] the latest forward
-    // sweep, [2] / [3] the same for the backward sweeps (+inf: none yet; see vpass)
-    double vg[MT ? 4 : 1][MT ? T : 1];
     union {
         double2 coef[2][K][T];   // [0]: (A1,A2)  [1]: (N0,W)   (precompute_lin_geom_generic)
         double vin[2][T];        // v-pass relaxation: published outgoing values
@@ -319,7 +348,8 @@ struct MinWaves {
 template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
 __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_kernel(KParams p) {
     constexpr int NW = T / 64;
-    __shared__ Smem<K, T, MT> sm;
+    constexpr bool WARM = WarmStart<T, MT>::value;
+    __shared__ Smem<K, T, WARM> sm;
 #ifdef RL_STAMPS
     unsigned long long st_acc[16] = {};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
@@ -388,19 +418,26 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 
     // ---- neighbour exchange (DPP in-wave, LDS across waves and for the wrap) ----
     // before a barrier: the wave's edge values (and the wrap value) go to LDS
-    double* const aF = &sm.pubF[0][(lane == 0) ? 64 + wid : lane];
-    double* const aL = &sm.pubL[0][(lane == 63) ? 64 + wid : lane];
-    double* const aW = &sm.pubW[0][(tid == Ta - 1) ? 64 : lane];
+    double* aF = nullptr;
+    double* aL = nullptr;
+    double* aW = nullptr;
+    if constexpr (NW > 1) {
+        aF = &sm.pubF[0][(lane == 0) ? 64 + wid : lane];
+        aL = &sm.pubL[0][(lane == 63) ? 64 + wid : lane];
+        aW = &sm.pubW[0][(tid == Ta - 1) ? 64 : lane];
+    }
     auto xpub = [&](int slot, const double (&a)[K]) RL_AI {
-        if constexpr (NW == 1) return;       // one wave: xget reads the edges with readlane
-        const double first = a[0], last = a[K - 1];
-        aF[slot * Smem<K, T, MT>::RF] = first;
-        aL[slot * Smem<K, T, MT>::RF] = last;
-        if (!RAGGED || cntL == K) {
-            aW[slot * 65] = last;
-        } else if (part_wave) {
-            const double lv = pick(a, cntL - 1);
-            if (tid == Ta - 1) sm.pubW[slot][64] = lv;
+        if constexpr (NW > 1) {              // one wave: xget reads the edges with readlane
+            constexpr int RF = PubTab<NW>::RF;
+            const double first = a[0], last = a[K - 1];
+            aF[slot * RF] = first;
+            aL[slot * RF] = last;
+            if (!RAGGED || cntL == K) {
+                aW[slot * 65] = last;
+            } else if (part_wave) {
+                const double lv = pick(a, cntL - 1);
+                if (tid == Ta - 1) sm.pubW[slot][64] = lv;
+            }
         }
     };
     // after the barrier: lv = value at sample base-1, rv = value at base+cnt (wrapped).
@@ -425,7 +462,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         // (one lane-masked select: a wave-uniform branch on tail_wave would be if-converted
         // into a second select pair)
         if (CLOSED) {
-            const double e0 = (NW == 1) ? ef : sm.pubF[slot][64];
+            double e0 = ef;
+            if constexpr (NW > 1) e0 = sm.pubF[slot][64];
             rv = wrap_lane ? e0 : rv;
         }
     };
@@ -643,17 +681,17 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // ---- v(s) profile: velocity_profile_forward_backward ref:782-862 ---------
     if (tid == 0) {
         VConst vc;
-        vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;   // ref:802-804
-        vc.a_total2 = vc.a_total * vc.a_total;
+        const double a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;   // ref:802-804
+        vc.a_total2 = a_total * a_total;
         vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;     // ref:810 constant prefix
         vc.Fr = C.mass_kg * 9.81 * C.c_rr;                   // ref:811
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
         vc.acc_cap = vs_cap(C.a_long_acc_cap); vc.brk_cap = vs_cap(C.a_long_brake_cap);
-        vc.h = h; vc.two_h = two_h;          // two_h = uni(2*h): the same value, from an SGPR pair
+        vc.h = h;
         vc.pw_free = power_never_binds(C.P_max_W, C.mass_kg, vc.kFd, vc.Fr, C.v_cap_mps, vc.acc_cap);
         sm.vc = vc;          // first read after the outer loop's first barrier
     }
-    if constexpr (MT) {      // v-pass warm starts: none yet (each thread reads only its own)
+    if constexpr (WARM) {    // v-pass warm starts: none yet (each thread reads only its own)
 #pragma unroll
         for (int j = 0; j < 4; ++j) sm.vg[j][tid] = INFINITY;
     }
@@ -694,7 +732,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             // rounds end only when every incoming value equals its neighbour's outgoing one --
             // and a start that is already exact leaves nothing to re-evaluate.
             {
-                const double g = MT ? sm.vg[MT && s == 0 ? 0 : MT ? 1 : 0][MT ? tid : 0] : INFINITY;
+                double g = INFINITY;
+                if constexpr (WARM) g = sm.vg[s == 0 ? 0 : 1][tid];
                 double in_prev = -1.0;       // sentinel (valid values are >= 0 or +inf)
                 double out = INFINITY;       // the value this chunk passes right
                 double wave_in = g;          // lane 0: the previous wave's last outgoing value
@@ -742,7 +781,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid > 0) wave_in = sm.u.vin[ro & 1][wid - 1];
                 }
-                if constexpr (MT) {
+                if constexpr (WARM) {
                     sm.vg[1][tid] = in_prev;
                     if (s == 0) sm.vg[0][tid] = in_prev;
                 }
@@ -763,7 +802,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 double vpre[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) vpre[k] = v[k];
-                const double g = MT ? sm.vg[MT && s == 0 ? 2 : MT ? 3 : 0][MT ? tid : 0] : INFINITY;   // warm start (as forward)
+                double g = INFINITY;                 // warm start (as forward)
+                if constexpr (WARM) g = sm.vg[s == 0 ? 2 : 3][tid];
                 double in_prev = -1.0;
                 double out = INFINITY;
                 double wave_in = g;          // lane 63: the next wave's first outgoing value
@@ -811,7 +851,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     if (!__syncthreads_or(pch || !conv) && ro > 0) break;
                     if (wid + 1 < NW) wave_in = sm.u.vin[ro & 1][wid + 1];
                 }
-                if constexpr (MT) {
+                if constexpr (WARM) {
                     sm.vg[3][tid] = in_prev;
                     if (s == 0) sm.vg[2][tid] = in_prev;
                 }

@@ -323,13 +323,13 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     // ---- v(s) profile (ref:782-862), contiguous ranges [t*Cr, t*Cr+Cr) --------
     if (tid == 0) {
         VConst vc;
-        vc.a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;
-        vc.a_total2 = vc.a_total * vc.a_total;
+        const double a_total = C.use_total_ge_lat ? smax(C.a_total_max, C.a_lat_max) : C.a_total_max;
+        vc.a_total2 = a_total * a_total;
         vc.kFd = 0.5 * C.rho_air * C.Cd * C.A_front_m2;
         vc.Fr = C.mass_kg * 9.81 * C.c_rr;
         vc.mass = C.mass_kg; vc.Pmax = C.P_max_W;
         vc.acc_cap = vs_cap(C.a_long_acc_cap); vc.brk_cap = vs_cap(C.a_long_brake_cap);
-        vc.h = h; vc.two_h = two_h;      // two_h = uni(2*h): the same value, from an SGPR pair
+        vc.h = h;
         vc.pw_free = power_never_binds(C.P_max_W, C.mass_kg, vc.kFd, vc.Fr, C.v_cap_mps, vc.acc_cap);
         sm.vc = vc;                      // first read after the outer loop's first barrier
     }
