@@ -1091,9 +1091,16 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #ifndef RL_A12_MT
 #define RL_A12_MT 0      // min-time: 0 none, 1 N0, 2 A1+A2, 3 all three in registers (A/B knob)
 #endif
-    constexpr bool A12R = (RL_A12_REG && !MT && (CLOSED || K < 8)) || (MT && CLOSED && (RL_A12_MT & 2));   // (A1, A2) in registers instead of LDS
-    constexpr bool N0R = (A12R && !MT && RL_A12_REG >= 2) || (MT && CLOSED && (RL_A12_MT & 1));            // and N0
-    double A1r[K], A2r[K], N0r[K];
+    // The latency shapes (K <= 2 samples per lane, registers to spare) hold all four
+    // coefficients in registers: no LDS read on the evaluation's dependency chain
+#ifndef RL_LAT_COEF_REG
+#define RL_LAT_COEF_REG 1
+#endif
+    constexpr bool ALLR = RL_LAT_COEF_REG && K <= 2;
+    constexpr bool A12R = ALLR || (RL_A12_REG && !MT && (CLOSED || K < 8)) || (MT && CLOSED && (RL_A12_MT & 2));   // (A1, A2) in registers instead of LDS
+    constexpr bool N0R = ALLR || (A12R && !MT && RL_A12_REG >= 2) || (MT && CLOSED && (RL_A12_MT & 1));            // and N0
+    constexpr bool WR = ALLR;                                                                                   // and W
+    double A1r[K], A2r[K], N0r[K], Wr[K];
 
     // One evaluation (eval_cost_grad_frozen ref:654-675 / _timeweighted ref:866-895)
     // of the trial vector a: J (uniform across the workgroup) and the Armijo
@@ -1122,7 +1129,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const double2 c01 = A12R ? make_double2(A1r[k], A2r[k]) : sm.u.coef[0][k][tid];   // (A1, A2)
-            const double2 c23 = N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
+            const double2 c23 = WR ? make_double2(N0r[k], Wr[k])
+                                : N0R ? make_double2(N0r[k], sm.u.coef[1][k][tid].y) : sm.u.coef[1][k][tid];   // (N0, W)
             double am = (k > 0) ? a[k - 1] : lv;
             double ap = (k + 1 < K) ? a[k + 1] : rv;
             double x1, x2;
@@ -1518,7 +1526,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 if (A12R) { A1r[k] = v ? a1 : 0.0; A2r[k] = v ? a2 : 0.0; }
                 if (N0R) N0r[k] = v ? n0 : 0.0;
                 else sm.u.coef[0][k][tid] = make_double2(v ? a1 : 0.0, v ? a2 : 0.0);
-                sm.u.coef[1][k][tid] = make_double2(v ? n0 : 0.0, v ? w : 0.0);
+                if (WR) Wr[k] = v ? w : 0.0;
+                else sm.u.coef[1][k][tid] = make_double2(v ? n0 : 0.0, v ? w : 0.0);
             }
         }
         RL_STAMP(3);

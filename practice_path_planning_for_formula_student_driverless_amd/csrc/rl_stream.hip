@@ -39,6 +39,20 @@ namespace {
 constexpr int TS = RL_STS;        // threads per instance
 constexpr int NWS = TS / 64;
 
+// The lane's first index of a strided pass, opaque to the optimiser: its addresses (array
+// base + 8·tid for each of the ~20 state arrays) are then formed inside the pass instead of
+// being hoisted to the kernel's start as 64-bit per-lane pointers live across every outer
+// iteration -- at the 128-VGPR budget of 1024 threads those were spilled and reloaded
+#ifndef RL_S_OPQ
+#define RL_S_OPQ 1
+#endif
+__device__ __forceinline__ int opq(int x) {
+#if RL_S_OPQ
+    asm volatile("" : "+v"(x));
+#endif
+    return x;
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_s(double x) {
     int lo = __double2loint(x), hi = __double2hiint(x);
@@ -335,12 +349,13 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     }
     for (int j = 0; j < 4; ++j) sm.vg[j][tid] = INFINITY;   // own entries only, read by this thread
     const int Cr = (N + TS - 1) / TS;
-    const int r0 = min(N, tid * Cr), r1 = min(N, r0 + Cr);
-    const bool ract = r0 < r1;
-    const bool has_left = ract && r0 > 0, has_right = ract && r1 < N;
+    const int r0_ = min(N, tid * Cr), r1_ = min(N, r0_ + Cr);
+    const bool ract = r0_ < r1_;
+    const bool has_left = ract && r0_ > 0, has_right = ract && r1_ < N;
     // (A/B, round 3: the register kernel's in-wave DPP relaxation made this kernel's C5
     // min-time run 5-15 % slower at every round cap tried -- one barrier per round stays)
     auto vpass = [&]() -> int {
+        const int r0 = opq(r0_), r1 = opq(r1_);   // (opaque: addresses formed per pass, see opq)
         const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
         for (int i = r0; i < r1; ++i) {
             double kk = fabs(KA[i]);
@@ -438,15 +453,18 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     auto vpass_reg = [&](auto crc, bool g2) -> int {
         constexpr int CR = decltype(crc)::value;
         const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
-        const int cnt = r1 - r0;                  // CR, except the last active thread; 0 beyond N
+        // (opaque: the chunk's addresses are formed here, not hoisted out of the outer loop
+        // as per-lane pointers for every instantiated CR, which were spilled)
+        const int rb = opq(r0_);
+        const int cnt = opq(r1_ - r0_);             // CR, except the last active thread; 0 beyond N
         // the chunk's curvatures stay in LDS (read-only for the whole v pass; each thread
         // reads only its own entries, so no barrier): in registers they spilled to scratch
         // (the 128-VGPR budget of 1024 threads), reloaded inside every step
-        double* const ka = &ska[r0];
+        double* const ka = &ska[rb];
         double v[CR];
 #pragma unroll
         for (int k = 0; k < CR; ++k) {
-            const double kv = (k < cnt) ? KA[r0 + k] : 0.0;
+            const double kv = (k < cnt) ? KA[rb + k] : 0.0;
             ka[k] = kv;                           // (the padding slots past N hold 0)
             const double kk = fabs(kv);
             const double vk = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
@@ -502,7 +520,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     if (s == 0) sm.vg[0][tid] = in_prev;
                 }
                 if (CLOSED) {                                  // ref:834-839
-                    if (ract && r1 == N) {
+                    if (ract && r1_ == N) {
                         double vl = v[0], kl = ka[0];
 #pragma unroll
                         for (int k = 1; k < CR; ++k)
@@ -559,7 +577,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 if (CLOSED) {                                  // ref:846-850
                     if (tid == 0) sm.bc[1] = vstep_bwd(vc, v[0], ka[0]);
                     __syncthreads();
-                    if (ract && r1 == N) {
+                    if (ract && r1_ == N) {
 #pragma unroll
                         for (int k = 0; k < CR; ++k)
                             if (k == cnt - 1) v[k] = smin(v[k], sm.bc[1]);
@@ -575,11 +593,11 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         if (g2) {
 #pragma unroll
             for (int k = 0; k < CR; ++k)
-                if (k < cnt) G2[r0 + k] = gamma2_of(ka[k], v[k], 0.0);
+                if (k < cnt) G2[rb + k] = gamma2_of(ka[k], v[k], 0.0);
         } else {
 #pragma unroll
             for (int k = 0; k < CR; ++k)
-                if (k < cnt) V[r0 + k] = v[k];
+                if (k < cnt) V[rb + k] = v[k];
         }
         return sweeps;
     };
@@ -599,7 +617,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     };
 
     // ---- init ---------------------------------------------------------------
-    for (int i = tid; i < N; i += TS) {
+    for (int i = opq(tid); i < N; i += TS) {
         X[i] = CEN[2 * i];
         Y[i] = CEN[2 * i + 1];
         ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0;   // (the gradient needs no zeroing: each outer
@@ -612,7 +630,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     for (int outer = 0;; ++outer) {
         __syncthreads();
         if (outer > 0) {                                           // ref:743-746
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 const double a = al_p[i];
                 ALAST[i] = a;
                 X[i] += NX[i] * a;
@@ -625,7 +643,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         RL_SSTAMP(5);
         if (outer < MO) {
             if (tid == 0) sm.ctr = 0;                              // read after the barrier below
-            for (int i = tid; i < N; i += TS) normal_at(i);
+            for (int i = opq(tid); i < N; i += TS) normal_at(i);
             __syncthreads();
             RL_SSTAMP(6);
             const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
@@ -668,7 +686,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 }
             }
 #else
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 corridor_at(i, guard);
                 if (outer == 0 && seed != 0)
                     al_p[i] = smin(HI[i], smax(LO[i], seed_value(seed, i, RL_SEED_SIGMA)));
@@ -680,7 +698,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
 #endif
         RL_SSTAMP(1);
         if ((MT && !RL_SFUSE) || outer == MO) {
-            for (int i = tid; i < N; i += TS) {                    // ref:595-620
+            for (int i = opq(tid); i < N; i += TS) {                    // ref:595-620
                 double xp, yp, xpp, ypp;
                 deriv(i, xp, yp, xpp, ypp);
                 KA[i] = (xp * ypp - yp * xpp) / pow15(smax(1e-12, xp * xp + yp * yp));
@@ -696,7 +714,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             __syncthreads();
             if (outer == MO) {
                 double lt[1] = {0.0};
-                for (int i = tid; i < N; i += TS) {                // ref:854-860
+                for (int i = opq(tid); i < N; i += TS) {                // ref:854-860
                     const int j = (i + 1 < N) ? i + 1 : (CLOSED ? 0 : i);
                     const double v0 = V[i], v1 = V[j];
                     p.ax[off + i] = (v1 * v1 - v0 * v0) / two_h;   // ref:857 (2.0*h)
@@ -709,18 +727,18 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 double v_avg = 0.0;
                 if (C.time_weight_use_inv_v) {
                     double vs[1] = {0.0};
-                    for (int i = tid; i < N; i += TS) vs[0] += V[i];
+                    for (int i = opq(tid); i < N; i += TS) vs[0] += V[i];
                     block_sum_s<1>(sm, vs, lane, wid);
                     v_avg = vs[0] / (double)(N > 1 ? N : 1);
                 }
-                for (int i = tid; i < N; i += TS) G2[i] = gamma2_of(KA[i], V[i], v_avg);   // ref:950-977
+                for (int i = opq(tid); i < N; i += TS) G2[i] = gamma2_of(KA[i], V[i], v_avg);   // ref:950-977
             }
         }
         RL_SSTAMP(2);
         if (outer == MO) break;
 
         if (!RL_SFUSE) {
-            for (int i = tid; i < N; i += TS) {                    // ref:622-651
+            for (int i = opq(tid); i < N; i += TS) {                    // ref:622-651
                 double xp, yp, xpp, ypp;
                 deriv(i, xp, yp, xpp, ypp);
                 const double nx = NX[i], ny = NY[i];
@@ -749,7 +767,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         // J; q1,q2,D1α to global for the gradient
         auto eval_j = [&](const double* a) -> double {
             double s3[2] = {0.0, 0.0};
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 const Term t = term_at(i, a[prev_i(i)], a[i], a[next_i(i)]);
                 Q1[i] = t.q1;
                 Q2[i] = t.q2;
@@ -768,7 +786,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         // stores α_trial, q1, q2 and D1α, which an accepted step needs.
         auto eval_trial = [&](double st, bool keep, double& dec) -> double {
             double s3[3] = {0.0, 0.0, 0.0};
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 const int im = prev_i(i), ip = next_i(i);
                 const double a0 = trial_at(i, st);
                 const double am = (im == i) ? a0 : trial_at(im, st);
@@ -785,7 +803,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         };
         // an accepted trial that was evaluated without `keep`: write what it would have
         auto materialize = [&](double st) {
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 const int im = prev_i(i), ip = next_i(i);
                 const double a0 = trial_at(i, st);
                 const double am = (im == i) ? a0 : trial_at(im, st);
@@ -796,7 +814,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             __syncthreads();
         };
         auto eval_grad = [&]() {
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 const int im = prev_i(i), ip = next_i(i);
                 const double g1 = d1t_at(i, Q1[im], Q1[i], Q1[ip]);
                 const double g2 = d2t_at(i, Q2[im], Q2[i], Q2[ip]);
@@ -820,7 +838,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             double s3[3 * MB];
 #pragma unroll
             for (int j = 0; j < 3 * MB; ++j) s3[j] = 0.0;
-            for (int i = tid; i < N; i += TS) {
+            for (int i = opq(tid); i < N; i += TS) {
                 const int im = prev_i(i), ip = next_i(i);
                 const double a0v = al_p[i], g0 = GR[i], lo0 = LO[i], hi0 = HI[i];
                 const double amv = al_p[im], gm = GR[im], lom = LO[im], him = HI[im];

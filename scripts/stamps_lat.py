@@ -32,10 +32,14 @@ for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n20
             f = (lib.rl_debug_stamps_mid if (K, T) == (4, 512) else
                  lib.rl_debug_stamps_lat if not thr else lib.rl_debug_stamps)
             assert f(st.ctypes.data_as(C.c_void_p), 1) == 0
+            o = abi.Outputs.alloc(1, prob.N, int(cfg.max_outer_iters), mode == 2)
+            c = o.as_c()
+            lib.rl_plan_fetch(h, C.byref(c) if mode == 1 else None, C.byref(c) if mode == 2 else None)
+            n_ev = int(np.asarray(o.evals).sum())
             tot = st.sum(0).astype(float)
             w0 = tot.sum() - (tot[12:16].sum() if VAR == "stamps" else 0.0)   # wave 0's own cycles
             print(f"{cname} N={prob.N} mode={mode} shape=({K},{T}) kernel {ms.value:.3f} ms (stamped); "
-                  f"wave-0 cycles {w0:.3e}: " +
+                  f"wave-0 cycles {w0:.3e}, {n_ev} evaluations ({w0 / max(n_ev, 1):.0f} cycles each, all phases): " +
                   ", ".join(f"{nm} {100 * tot[i] / w0:.1f}%" for i, nm in enumerate(names) if tot[i] > 0), flush=True)
             lib.rl_plan_destroy(h)
 os.environ.pop("RL_LAT_SHAPES", None)
