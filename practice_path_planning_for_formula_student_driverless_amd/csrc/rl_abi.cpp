@@ -504,11 +504,7 @@ static int alloc_mode(rl_plan* p, int m) {
             return rc;
     }
     if (p->stream) {
-        double** arrs[rl::RL_STREAM_ARRAYS] = {&mb.sb.al, &mb.sb.an, &mb.sb.gr, &mb.sb.lo, &mb.sb.hi,
-                                              &mb.sb.a1, &mb.sb.a2, &mb.sb.n0, &mb.sb.w, &mb.sb.q1,
-                                              &mb.sb.q2, &mb.sb.d1, &mb.sb.g2, &mb.sb.v, &mb.sb.vs};
-        for (auto a : arrs)
-            if ((rc = p->alloc(a, BN))) return rc;
+        if ((rc = p->alloc(&mb.sb.base, BN * rl::RL_STREAM_ARRAYS))) return rc;   // [B][15][N]
     }
     return RL_OK;
 }

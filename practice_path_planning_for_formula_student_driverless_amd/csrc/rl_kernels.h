@@ -28,9 +28,12 @@ struct KParams {
     double L, veh_width;
 };
 
-// Per-instance HBM state of the large-N streaming kernel (rl_stream.hip), [B][N] each.
+// Per-instance HBM state of the large-N streaming kernel (rl_stream.hip): RL_STREAM_ARRAYS
+// arrays of N doubles per instance, instance-major [B][RL_STREAM_ARRAYS][N] in one allocation
+// (al, an, gr, lo, hi, a1, a2, n0, w, q1, q2, d1, g2, v, vs), so one buffer resource and a
+// field offset address any of an instance's arrays.
 struct StreamBufs {
-    double *al, *an, *gr, *lo, *hi, *a1, *a2, *n0, *w, *q1, *q2, *d1, *g2, *v, *vs;
+    double* base;
 };
 constexpr int RL_STREAM_ARRAYS = 15;
 constexpr int RL_REG_MAX_N = 4096;          // register-resident kernel covers N <= 4096

@@ -53,6 +53,47 @@ __device__ __forceinline__ int opq(int x) {
     return x;
 }
 
+// The instance's state arrays (StreamBufs: [B][15][N] in one allocation) through one buffer
+// resource: a load / store takes the resource (4 SGPRs, one per instance), the array's byte
+// offset (an SGPR) and the lane's byte offset i*8 (one VGPR shared by every array indexed by i).
+// As plain pointers each array's 64-bit base held an SGPR pair for the whole kernel (30 of its
+// 106 SGPRs for these 15 arrays) and the kernel spilled SGPRs to VGPR lanes, VGPRs to scratch.
+// Offsets stay below 2^31: 15 * N * 8 B with N <= RL_STREAM_MAX_N.  A/B knob: 0 = pointers.
+#ifndef RL_S_BUF
+#define RL_S_BUF 1
+#endif
+#ifndef RL_S_BUF_OPQ
+#define RL_S_BUF_OPQ 1
+#endif
+typedef unsigned int u32x2_s __attribute__((ext_vector_type(2)));
+struct BufArr {
+    __amdgpu_buffer_rsrc_t r;
+    int so;                     // byte offset of the array within the instance's resource
+    struct Ref {
+        __amdgpu_buffer_rsrc_t r;
+        int so, vo;
+        __device__ __forceinline__ operator double() const {
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+        }
+        __device__ __forceinline__ Ref& operator=(double v) {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_s, v), r, vo, so, 0);
+            return *this;
+        }
+        __device__ __forceinline__ Ref& operator=(const Ref& o) { return *this = (double)o; }   // a store, not a copy
+        __device__ __forceinline__ Ref& operator+=(double v) { return *this = (double)*this + v; }
+    };
+    __device__ __forceinline__ Ref operator[](int i) const {
+#if RL_S_BUF_OPQ
+        int n8 = so;            // (so holds N*8 and k: field k's offset formed at each access)
+        asm volatile("" : "+s"(n8));
+        return Ref{r, k * n8, i * 8};
+#else
+        return Ref{r, so, i * 8};
+#endif
+    }
+    int k;
+};
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_s(double x) {
     int lo = __double2loint(x), hi = __double2hiint(x);
@@ -119,6 +160,7 @@ struct SSmem {
     // sweep, [2] / [3] the same for the backward sweeps (+inf: none yet)
     double vg[4][TS];
     double bc[4];
+    double* pp[7];    // the instance's output arrays X .. KA (RL_S_PLDS), read where used
     VConst vc;        // v-pass constants (read at the start of each v pass: no registers held)
     int ctr;          // corridor work queue: next chunk of 64*RL_SCK samples
 };
@@ -165,6 +207,28 @@ __device__ unsigned long long rl_dbg_stamps_s[16384][16];
 #define RL_SSTAMP(slot) do {} while (0)
 #endif
 
+// the output arrays' bases: 0 pointers held for the whole kernel, 1 all seven in an LDS table
+// read where used, 2 X, Y, NX, NY held (every pass reads them) and alpha_total, alpha_last,
+// kappa from the table (once-per-outer passes).  C5 A/B (profiles/r05/ab_c5_scratch.log):
+// min-time scratch 112 / 64 / 32 B/lane, 32.3 / 32.7 / 32.2 ms (round-5 head 160 B/lane, 32.3)
+#ifndef RL_S_PLDS
+#define RL_S_PLDS 2
+#endif
+// a uniform pointer read from LDS, as an SGPR pair
+template <class T>
+__device__ __forceinline__ T* unip(T* q) {
+    const uint64_t u = (uint64_t)q;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+#if RL_S_PLDS == 2
+#define PPT(k) ((k) < 4 ? PL4[(k) & 3] : unip(sm.pp[(k)]))
+#elif RL_S_PLDS
+#define PPT(k) (unip(sm.pp[(k)]))
+#else
+#define PPT(k) (((double* const[]){X, Y, NX, NY, ATOT, ALAST, KA})[(k)])
+#endif
+
 template <bool CLOSED, bool MT>
 // RL_STS_MINW: minimum waves per SIMD the register budget must allow (0: the compiler's
 // choice for TS), e.g. TS = 512 with 4 keeps two instances co-resident per CU (A/B knob)
@@ -199,28 +263,42 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     const double lam = C.lambda_smooth, lam2 = uni(2.0 * lam);
 
     const size_t off = (size_t)b * (size_t)N;
+#if RL_S_PLDS
+    // the output arrays' bases in LDS, read where they are used: held for the whole kernel they
+    // sat in VGPR pairs (no SGPRs left) and were spilled (RL_S_PLDS above)
+    if (tid == 0) {
+        sm.pp[0] = p.x + off; sm.pp[1] = p.y + off; sm.pp[2] = p.nx + off; sm.pp[3] = p.ny + off;
+        sm.pp[4] = p.alpha_total + off; sm.pp[5] = p.alpha_last + off; sm.pp[6] = p.kappa + off;
+    }
+    __syncthreads();
+#if RL_S_PLDS == 2
+    double* const PL4[4] = {p.x + off, p.y + off, p.nx + off, p.ny + off};   // (the corridor's, held)
+#endif
+#else
     double* __restrict__ X = p.x + off;
     double* __restrict__ Y = p.y + off;
     double* __restrict__ NX = p.nx + off;
     double* __restrict__ NY = p.ny + off;
     double* __restrict__ ATOT = p.alpha_total + off;
     double* __restrict__ ALAST = p.alpha_last + off;
-    double* __restrict__ AL = sb.al + off;
-    double* __restrict__ AN = sb.an + off;               // α and α_trial swap roles on accept
-    double* __restrict__ GR = sb.gr + off;
-    double* __restrict__ LO = sb.lo + off;
-    double* __restrict__ HI = sb.hi + off;
-    double* __restrict__ CA1 = sb.a1 + off;
-    double* __restrict__ CA2 = sb.a2 + off;
-    double* __restrict__ CN0 = sb.n0 + off;
-    double* __restrict__ CW = sb.w + off;
-    double* __restrict__ Q1 = sb.q1 + off;
-    double* __restrict__ Q2 = sb.q2 + off;
-    double* __restrict__ D1 = sb.d1 + off;
-    double* __restrict__ G2 = sb.g2 + off;
     double* __restrict__ KA = p.kappa + off;          // κ scratch, final output at the end
-    double* __restrict__ V = sb.v + off;
-    double* __restrict__ VS = sb.vs + off;
+#endif
+    // the streaming state ([B][15][N], StreamBufs); al / an swap roles on every accepted step
+#if RL_S_BUF
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        sb.base + (size_t)b * RL_STREAM_ARRAYS * (size_t)N, (short)0, RL_STREAM_ARRAYS * N * 8, 0x00020000);
+#if RL_S_BUF_OPQ
+    auto sfield = [&](int k) { return BufArr{srs, N * 8, k}; };
+#else
+    auto sfield = [&](int k) { return BufArr{srs, k * N * 8, k}; };
+#endif
+#else
+    double* const sinst = sb.base + (size_t)b * RL_STREAM_ARRAYS * (size_t)N;
+    auto sfield = [&](int k) -> double* __restrict__ { return sinst + (size_t)k * N; };
+#endif
+    const auto AL = sfield(0), AN = sfield(1), GR = sfield(2), LO = sfield(3), HI = sfield(4);
+    const auto CA1 = sfield(5), CA2 = sfield(6), CN0 = sfield(7), CW = sfield(8);
+    const auto Q1 = sfield(9), Q2 = sfield(10), D1 = sfield(11), G2 = sfield(12), V = sfield(13), VS = sfield(14);
 
     // neighbour index i-1 / i+1: wrapped when closed, clamped when open (no integer division)
     auto prev_i = [&](int i) -> int { return i > 0 ? i - 1 : (CLOSED ? N - 1 : 0); };
@@ -230,36 +308,36 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         if (N == 1) { xp = 1; yp = 0; xpp = ypp = 0; return; }
         if (CLOSED) {
             const int ip = next_i(i), im = prev_i(i);
-            xp = (X[ip] - X[im]) / two_h; yp = (Y[ip] - Y[im]) / two_h;
-            xpp = (sub2x(X[ip], X[i]) + X[im]) / hh; ypp = (sub2x(Y[ip], Y[i]) + Y[im]) / hh;
+            xp = (PPT(0)[ip] - PPT(0)[im]) / two_h; yp = (PPT(1)[ip] - PPT(1)[im]) / two_h;
+            xpp = (sub2x(PPT(0)[ip], PPT(0)[i]) + PPT(0)[im]) / hh; ypp = (sub2x(PPT(1)[ip], PPT(1)[i]) + PPT(1)[im]) / hh;
         } else if (i == 0) {
-            xp = (X[1] - X[0]) / h; yp = (Y[1] - Y[0]) / h;
-            if (N >= 3) { xpp = (sub2x(X[2], X[1]) + X[0]) / hh; ypp = (sub2x(Y[2], Y[1]) + Y[0]) / hh; }
+            xp = (PPT(0)[1] - PPT(0)[0]) / h; yp = (PPT(1)[1] - PPT(1)[0]) / h;
+            if (N >= 3) { xpp = (sub2x(PPT(0)[2], PPT(0)[1]) + PPT(0)[0]) / hh; ypp = (sub2x(PPT(1)[2], PPT(1)[1]) + PPT(1)[0]) / hh; }
             else xpp = ypp = 0;
         } else if (i == N - 1) {
-            xp = (X[N - 1] - X[N - 2]) / h; yp = (Y[N - 1] - Y[N - 2]) / h;
-            if (N >= 3) { xpp = (sub2x(X[N - 1], X[N - 2]) + X[N - 3]) / hh; ypp = (sub2x(Y[N - 1], Y[N - 2]) + Y[N - 3]) / hh; }
+            xp = (PPT(0)[N - 1] - PPT(0)[N - 2]) / h; yp = (PPT(1)[N - 1] - PPT(1)[N - 2]) / h;
+            if (N >= 3) { xpp = (sub2x(PPT(0)[N - 1], PPT(0)[N - 2]) + PPT(0)[N - 3]) / hh; ypp = (sub2x(PPT(1)[N - 1], PPT(1)[N - 2]) + PPT(1)[N - 3]) / hh; }
             else xpp = ypp = 0;
         } else {
-            xp = (X[i + 1] - X[i - 1]) / two_h; yp = (Y[i + 1] - Y[i - 1]) / two_h;
-            xpp = (sub2x(X[i + 1], X[i]) + X[i - 1]) / hh; ypp = (sub2x(Y[i + 1], Y[i]) + Y[i - 1]) / hh;
+            xp = (PPT(0)[i + 1] - PPT(0)[i - 1]) / two_h; yp = (PPT(1)[i + 1] - PPT(1)[i - 1]) / two_h;
+            xpp = (sub2x(PPT(0)[i + 1], PPT(0)[i]) + PPT(0)[i - 1]) / hh; ypp = (sub2x(PPT(1)[i + 1], PPT(1)[i]) + PPT(1)[i - 1]) / hh;
         }
     };
     // normals_from_points_generic ref:581-593
     auto normal_at = [&](int i) {
         double tx, ty;
         if (N == 1) { tx = 1; ty = 0; }
-        else if (CLOSED) { const int ip = next_i(i), im = prev_i(i); tx = (X[ip] - X[im]) * 0.5; ty = (Y[ip] - Y[im]) * 0.5; }
-        else if (i == 0) { tx = X[1] - X[0]; ty = Y[1] - Y[0]; }
-        else if (i == N - 1) { tx = X[N - 1] - X[N - 2]; ty = Y[N - 1] - Y[N - 2]; }
-        else { tx = (X[i + 1] - X[i - 1]) * 0.5; ty = (Y[i + 1] - Y[i - 1]) * 0.5; }
+        else if (CLOSED) { const int ip = next_i(i), im = prev_i(i); tx = (PPT(0)[ip] - PPT(0)[im]) * 0.5; ty = (PPT(1)[ip] - PPT(1)[im]) * 0.5; }
+        else if (i == 0) { tx = PPT(0)[1] - PPT(0)[0]; ty = PPT(1)[1] - PPT(1)[0]; }
+        else if (i == N - 1) { tx = PPT(0)[N - 1] - PPT(0)[N - 2]; ty = PPT(1)[N - 1] - PPT(1)[N - 2]; }
+        else { tx = (PPT(0)[i + 1] - PPT(0)[i - 1]) * 0.5; ty = (PPT(1)[i + 1] - PPT(1)[i - 1]) * 0.5; }
         if (sqrt(tx * tx + ty * ty) < 1e-15) { tx = 1; ty = 0; }
         double vx = -ty, vy = tx;
         double n = sqrt(vx * vx + vy * vy);
         double ox = 0, oy = 0;
         if (!(n < 1e-15)) { ox = vx / n; oy = vy / n; }
-        NX[i] = ox;
-        NY[i] = oy;
+        PPT(2)[i] = ox;
+        PPT(3)[i] = oy;
 #if RL_SFUSE
         // precompute_lin_geom_generic (ref:622-651) at i in the same pass over P: it needs
         // only this sample's normal, so the later lin-geom pass (and, for min-time, the
@@ -272,12 +350,12 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         CN0[i] = n0;
         const double d = pow15(smax(1e-12, xp * xp + yp * yp));
         CW[i] = 1.0 / d;
-        if (MT) KA[i] = n0 / d;
+        if (MT) PPT(6)[i] = n0 / d;
 #endif
     };
     // corridor (ref:694-711 / 749-756) at sample i via the per-lane candidate scan
     auto corridor_at = [&](int i, double guard) {
-        const double qx[1] = {X[i]}, qy[1] = {Y[i]}, ux[1] = {NX[i]}, uy[1] = {NY[i]};
+        const double qx[1] = {PPT(0)[i]}, qy[1] = {PPT(1)[i]}, ux[1] = {PPT(2)[i]}, uy[1] = {PPT(3)[i]};
         const bool act[1] = {true};
         double lk[1], hk[1];
         corridor_bounds<1>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
@@ -358,7 +436,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         const int r0 = opq(r0_), r1 = opq(r1_);   // (opaque: addresses formed per pass, see opq)
         const VConst vc = RL_VC_UNI ? vconst_uniform(sm.vc) : sm.vc;
         for (int i = r0; i < r1; ++i) {
-            double kk = fabs(KA[i]);
+            double kk = fabs(PPT(6)[i]);
             V[i] = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
         }
         int sweeps = 0;
@@ -379,10 +457,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     double cur = has_left ? smin(VS[r0], in) : VS[r0];
                     V[r0] = cur;
                     for (int i = r0; i + 1 < r1; ++i) {
-                        cur = smin(VS[i + 1], vstep_fwd(vc, cur, KA[i]));
+                        cur = smin(VS[i + 1], vstep_fwd(vc, cur, PPT(6)[i]));
                         V[i + 1] = cur;
                     }
-                    if (has_right) sm.u.vin[it & 1][tid] = vstep_fwd(vc, cur, KA[r1 - 1]);
+                    if (has_right) sm.u.vin[it & 1][tid] = vstep_fwd(vc, cur, PPT(6)[r1 - 1]);
                 } else if (has_right) {
                     sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
                 }
@@ -393,7 +471,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 if (s == 0) sm.vg[0][tid] = in_prev;
             }
             if (CLOSED) {                                          // ref:834-839
-                if (ract && r1 == N) sm.bc[0] = vstep_fwd(vc, V[N - 1], KA[N - 1]);
+                if (ract && r1 == N) sm.bc[0] = vstep_fwd(vc, V[N - 1], PPT(6)[N - 1]);
                 __syncthreads();
                 if (tid == 0) V[0] = smin(V[0], sm.bc[0]);
                 __syncthreads();
@@ -413,10 +491,10 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     double cur = has_right ? smin(Q1[r1 - 1], in) : Q1[r1 - 1];
                     V[r1 - 1] = cur;
                     for (int i = r1 - 2; i >= r0; --i) {
-                        cur = smin(Q1[i], vstep_bwd(vc, cur, KA[i + 1]));
+                        cur = smin(Q1[i], vstep_bwd(vc, cur, PPT(6)[i + 1]));
                         V[i] = cur;
                     }
-                    if (has_left) sm.u.vin[it & 1][tid] = vstep_bwd(vc, cur, KA[r0]);
+                    if (has_left) sm.u.vin[it & 1][tid] = vstep_bwd(vc, cur, PPT(6)[r0]);
                 } else if (has_left) {
                     sm.u.vin[it & 1][tid] = sm.u.vin[(it - 1) & 1][tid];
                 }
@@ -427,7 +505,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 if (s == 0) sm.vg[2][tid] = in_prev;
             }
             if (CLOSED) {                                          // ref:846-850
-                if (tid == 0) sm.bc[1] = vstep_bwd(vc, V[0], KA[0]);
+                if (tid == 0) sm.bc[1] = vstep_bwd(vc, V[0], PPT(6)[0]);
                 __syncthreads();
                 if (ract && r1 == N) V[N - 1] = smin(V[N - 1], sm.bc[1]);
                 __syncthreads();
@@ -464,7 +542,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         double v[CR];
 #pragma unroll
         for (int k = 0; k < CR; ++k) {
-            const double kv = (k < cnt) ? KA[rb + k] : 0.0;
+            const double kv = (k < cnt) ? PPT(6)[rb + k] : 0.0;
             ka[k] = kv;                           // (the padding slots past N hold 0)
             const double kk = fabs(kv);
             const double vk = smin(C.v_cap_mps, sqrt(C.a_lat_max / smax(kk, C.kappa_eps)));   // ref:787-794
@@ -618,24 +696,24 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
 
     // ---- init ---------------------------------------------------------------
     for (int i = opq(tid); i < N; i += TS) {
-        X[i] = CEN[2 * i];
-        Y[i] = CEN[2 * i + 1];
-        ATOT[i] = 0.0; ALAST[i] = 0.0; AL[i] = 0.0;   // (the gradient needs no zeroing: each outer
+        PPT(0)[i] = CEN[2 * i];
+        PPT(1)[i] = CEN[2 * i + 1];
+        PPT(4)[i] = 0.0; PPT(5)[i] = 0.0; AL[i] = 0.0;   // (the gradient needs no zeroing: each outer
     }                                                     // iteration's first evaluation writes it first)
     const int MO = C.max_outer_iters;
     bool first_batch = RL_BT_ADAPT ? false : (RL_BT_FIRST && (!MT || RL_BT_FIRST_MT));
-    double* al_p = AL;
-    double* an_p = AN;
+    auto al_p = AL;
+    auto an_p = AN;
     RL_SSTAMP(0);
     for (int outer = 0;; ++outer) {
         __syncthreads();
         if (outer > 0) {                                           // ref:743-746
             for (int i = opq(tid); i < N; i += TS) {
                 const double a = al_p[i];
-                ALAST[i] = a;
-                X[i] += NX[i] * a;
-                Y[i] += NY[i] * a;
-                ATOT[i] += a;
+                PPT(5)[i] = a;
+                PPT(0)[i] += PPT(2)[i] * a;
+                PPT(1)[i] += PPT(3)[i] * a;
+                PPT(4)[i] += a;
                 al_p[i] = 0.0;                                     // ref:757
             }
             __syncthreads();
@@ -664,7 +742,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
 #pragma unroll
                 for (int k = 0; k < RL_SCK; ++k) {
                     const int i = min(i0 + k, N - 1);
-                    qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
+                    qx[k] = PPT(0)[i]; qy[k] = PPT(1)[i]; ux[k] = PPT(2)[i]; uy[k] = PPT(3)[i];
                     act[k] = i0 + k < N;
                 }
 #ifdef RL_STAMPS
@@ -701,7 +779,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             for (int i = opq(tid); i < N; i += TS) {                    // ref:595-620
                 double xp, yp, xpp, ypp;
                 deriv(i, xp, yp, xpp, ypp);
-                KA[i] = (xp * ypp - yp * xpp) / pow15(smax(1e-12, xp * xp + yp * yp));
+                PPT(6)[i] = (xp * ypp - yp * xpp) / pow15(smax(1e-12, xp * xp + yp * yp));
                 if (outer == MO) p.heading[off + i] = MT ? atan2_stream(yp, xp) : atan2_cr(yp, xp);   // ref:616
             }
             __syncthreads();
@@ -731,7 +809,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     block_sum_s<1>(sm, vs, lane, wid);
                     v_avg = vs[0] / (double)(N > 1 ? N : 1);
                 }
-                for (int i = opq(tid); i < N; i += TS) G2[i] = gamma2_of(KA[i], V[i], v_avg);   // ref:950-977
+                for (int i = opq(tid); i < N; i += TS) G2[i] = gamma2_of(PPT(6)[i], V[i], v_avg);   // ref:950-977
             }
         }
         RL_SSTAMP(2);
@@ -741,7 +819,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
             for (int i = opq(tid); i < N; i += TS) {                    // ref:622-651
                 double xp, yp, xpp, ypp;
                 deriv(i, xp, yp, xpp, ypp);
-                const double nx = NX[i], ny = NY[i];
+                const double nx = PPT(2)[i], ny = PPT(3)[i];
                 CA1[i] = nx * ypp - ny * xpp;
                 CA2[i] = xp * ny - yp * nx;
                 CN0[i] = xp * ypp - yp * xpp;
@@ -765,7 +843,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         };
         // one evaluation of the vector `a` (already written and synchronised):
         // J; q1,q2,D1α to global for the gradient
-        auto eval_j = [&](const double* a) -> double {
+        auto eval_j = [&](const auto a) -> double {
             double s3[2] = {0.0, 0.0};
             for (int i = opq(tid); i < N; i += TS) {
                 const Term t = term_at(i, a[prev_i(i)], a[i], a[next_i(i)]);
@@ -900,7 +978,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                         if (RL_BT_ADAPT && kept && j == 0) first_batch = !(Jn[0] <= J + C.armijo_c * dn[0]);
                         if (Jn[j] <= J + C.armijo_c * dn[j]) {
                             if (!(kept && j == 0)) materialize(st[j]);
-                            double* t = al_p; al_p = an_p; an_p = t;
+                            const auto t = al_p; al_p = an_p; an_p = t;
                             eval_grad();
                             J = Jn[j];
                             accepted = true;
@@ -923,7 +1001,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                 if (RL_BT_ADAPT && keep) first_batch = !(Jn <= J + C.armijo_c * dec);
                 if (Jn <= J + C.armijo_c * dec) {
                     if (!keep) materialize(step);
-                    double* t = al_p; al_p = an_p; an_p = t;       // α := α_trial (uniform swap)
+                    const auto t = al_p; al_p = an_p; an_p = t;       // α := α_trial (uniform swap)
                     eval_grad();
                     J = Jn;
                     accepted = true;
@@ -972,6 +1050,8 @@ static hipError_t launch_s(const KParams& p, const StreamBufs& sb, hipStream_t s
     hipLaunchKernelGGL((rl_stream_kernel<CL, MT>), dim3(p.B), dim3(TS), 0, st, p, sb);
     return hipGetLastError();
 }
+
+#undef PPT
 
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st) {
     if (p.N <= 0 || p.N > RL_STREAM_MAX_N) return hipErrorInvalidValue;
