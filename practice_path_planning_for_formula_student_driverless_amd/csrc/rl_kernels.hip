@@ -37,6 +37,7 @@ static hipError_t launch_ktm(const KParams& p, hipStream_t st) {
 // variant table by N: (K samples per lane, T lanes per instance)
 //   throughput shapes (every batch that fills the GPU):
 //   N <= 256          (4, 64)      one wave per instance
+//   N <= 320          (5, 64)      one wave per instance (RL_S5)
 //   N <= 512          (8, 64)      one wave per instance
 //   N <= 1024         (8, 128)
 //   N <= 2048         (RL_MID_K, RL_MID_T)   default (8, 256); min-time (RL_MIDMT_K, RL_MIDMT_T) = (4, 512)
@@ -47,8 +48,16 @@ static hipError_t launch_ktm(const KParams& p, hipStream_t st) {
 //   one instance over a whole CU -- the drop-in use, one track per call (ref:1347, 1397)
 static_assert(RL_MID_K * RL_MID_T == 2048, "mid variant must cover N <= 2048");
 static_assert(RL_MIDMT_K == 4 && RL_MIDMT_T == 512, "the mid min-time shape is (4, 512), instantiated in rl_kernels_lat.hip");
+// (5, 64) for 256 < N <= 320 (testday1/3 of the bundled tracks): one wave, 5 samples per lane
+// instead of 8, 0 B scratch and two waves per SIMD in both modes.  C4 (scripts/ab_c4_single.py,
+// profiles/r05/ab_c4_s5.log): those plans alone min-time 4.16 / 4.59 -> 3.32 / 3.74 ms,
+// min-curv 3.64 / 3.97 -> 3.07 / 3.36 ms; the concurrent sweep 17.55 -> 16.42 ms, bit-exact
+#ifndef RL_S5
+#define RL_S5 1
+#endif
 int pick_k(int N) {
     if (N <= 4 * 64) return 4;
+    if (RL_S5 && N <= 5 * 64) return 5;
     if (N <= 8 * 64) return 8;
     if (N <= 8 * 128) return 8;
     if (N <= 2048) return RL_MID_K;
@@ -77,6 +86,7 @@ Shape pick_shape(int N, int B, bool mintime, int cus) {
     const Shape lat = lat_shape(N);
     if (lat.K > 0 && lat_shapes_enabled() && (int64_t)B * (lat.T / 64) <= (int64_t)4 * cus) return lat;
     if (N <= 4 * 64) return {4, 64};
+    if (RL_S5 && N <= 5 * 64) return {5, 64};
     if (N <= 8 * 64) return {8, 64};
     if (N <= 8 * 128) return {8, 128};
     if (N <= 2048) {
@@ -102,6 +112,9 @@ hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     const Shape lat = lat_shape(p.N);
     if ((s.K == lat.K && s.T == lat.T) || (s.K == 4 && s.T == 512)) return launch_optimize_lat(p, mintime, st);
     if (s.K == 4 && s.T == 64) return launch_kt<4, 64>(p, mintime, st);
+#if RL_S5
+    if (s.K == 5 && s.T == 64) return launch_kt<5, 64>(p, mintime, st);
+#endif
     if (s.K == 8 && s.T == 64) return launch_kt<8, 64>(p, mintime, st);      // one wave (single-wave paths)
     if (s.K == 8 && s.T == 128) return launch_kt<8, 128>(p, mintime, st);
     if (p.N <= 2048) {

@@ -131,8 +131,9 @@ def test_kernel_shape_table():
     assert abi.kernel_shape(216, 257, MC) == (4, 64)
     assert abi.kernel_shape(261, 1, MT) == (1, 320)
     assert abi.kernel_shape(261, 204, MC) == (1, 320)
-    assert abi.kernel_shape(261, 205, MC) == (8, 64)
-    assert abi.kernel_shape(261, 512, MT) == (8, 64)
+    assert abi.kernel_shape(261, 205, MC) == (5, 64)
+    assert abi.kernel_shape(261, 512, MT) == (5, 64)
+    assert abi.kernel_shape(400, 512, MT) == (8, 64)
     assert abi.kernel_shape(392, 1, MC) == (1, 448)
     assert abi.kernel_shape(512, 1, MT) == (1, 512)
     assert abi.kernel_shape(2000, 1, MC) == (4, 512)
