@@ -17,7 +17,7 @@ if VAR == "stamps":     # VSPLIT (min-time, K = 1): slot 11 = wave 0's join wait
     names[11], names[12] = "vsplit: join wait + collect (wave 0)", "vsplit: v-pass wave's v-pass [not in the sum]"
     names[13], names[14], names[15] = ("vsplit: wave 0 scan [in 7-10]", "vsplit: wave 1 scan [not in the sum]",
                                        "vsplit: wave 2 scan [not in the sum]")
-for cname in ("track_training_map", "track_competition_map_testday3", "cmap1_n2000"):
+for cname in [c for c in os.environ.get("ST_CASES", "track_training_map,track_competition_map_testday3,cmap1_n2000").split(",")]:
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)
     for mode in (1, 2):
         for thr in (False, True):
