@@ -383,6 +383,32 @@ def test_streaming_kernel_golden_tracks(monkeypatch):
         assert abs(mt.lap[0] - float(case["mt_lap"])) / float(case["mt_lap"]) <= REL
 
 
+def _pick(o: abi.Outputs, rows) -> abi.Outputs:
+    return abi.Outputs(**{f: (None if getattr(o, f) is None else getattr(o, f)[rows])
+                          for f in o.__dataclass_fields__})
+
+
+def test_streaming_state_beyond_4gib():
+    """The streaming kernel's state ([B][15][N] in one allocation, reached through one buffer
+    resource per instance with 32-bit offsets) for instances whose state starts past 4 GiB:
+    the first and the last instances equal the oracle."""
+    _lib_or_skip()
+    N = 8192
+    per_inst = 15 * N * 8
+    B = (4 << 30) // per_inst + 3            # the last two instances' state starts past 4 GiB
+    assert (B - 2) * per_inst > (4 << 30)
+    prob = _synthetic(N, True, np.random.default_rng(5))
+    cfg = abi.default_cfg()
+    cfg.max_outer_iters = 1
+    cfg.max_inner_iters = 3
+    seeds = np.arange(B, dtype=np.uint64)
+    mc, mt = raceline.optimize_batch(prob, cfg, seeds, B)
+    rows = [0, B - 2, B - 1]
+    omc, omt = O.run_oracle(prob, cfg, seeds=seeds[rows], B=len(rows))
+    compare_outputs(_pick(mc, rows), omc, False, "stream 4GiB.mc")
+    compare_outputs(_pick(mt, rows), omt, True, "stream 4GiB.mt")
+
+
 GEOM = list(O.manifest().get("geom_cases", {}))
 
 
