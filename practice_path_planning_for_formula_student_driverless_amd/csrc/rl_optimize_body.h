@@ -1089,7 +1089,10 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #define RL_A12_REG 2
 #endif
 #ifndef RL_A12_MT
-#define RL_A12_MT 0      // min-time: 0 none, 1 N0, 2 A1+A2, 3 all three in registers (A/B knob)
+// min-time, shapes of 256+ lanes: 0 none, 1 N0, 2 A1+A2, 3 all three in registers.  2: C3
+// (B = 4096, (8, 256)) min-time 39.19 -> 38.77 ms at 32 B/lane of scratch outside the loop,
+// B = 256 ((4, 512)) 7.50 -> 7.34 ms, bit-exact (profiles/r05/ab_c3_a12mt.log)
+#define RL_A12_MT 2
 #endif
     // The latency shapes (K <= 2 samples per lane, registers to spare) hold all four
     // coefficients in registers: no LDS read on the evaluation's dependency chain
@@ -1097,8 +1100,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #define RL_LAT_COEF_REG 1
 #endif
     constexpr bool ALLR = RL_LAT_COEF_REG && K <= 2;
-    constexpr bool A12R = ALLR || (RL_A12_REG && !MT && (CLOSED || K < 8)) || (MT && CLOSED && (RL_A12_MT & 2));   // (A1, A2) in registers instead of LDS
-    constexpr bool N0R = ALLR || (A12R && !MT && RL_A12_REG >= 2) || (MT && CLOSED && (RL_A12_MT & 1));            // and N0
+    constexpr bool A12R = ALLR || (RL_A12_REG && !MT && (CLOSED || K < 8)) || (MT && CLOSED && T >= 256 && (RL_A12_MT & 2));   // (A1, A2) in registers instead of LDS
+    constexpr bool N0R = ALLR || (A12R && !MT && RL_A12_REG >= 2) || (MT && CLOSED && T >= 256 && (RL_A12_MT & 1));            // and N0
     constexpr bool WR = ALLR;                                                                                   // and W
     double A1r[K], A2r[K], N0r[K], Wr[K];
 
