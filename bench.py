@@ -169,6 +169,27 @@ def reference_multicore(prob, cfg, cores, work: str, MO: int, budget_s: float = 
                     f"single-threaded"}
 
 
+def cpu_multicore_leg() -> dict:
+    """Context only (SURVEY §8d optional): the reference instance-parallel on
+    this GPU's host CPU share -- one ref_bench process per core, each pinned, on C2's
+    problem.  Run by the CPU-leg child only when the parent says so, after every GPU leg
+    (it saturates 16 cores, which must not overlap any rank's GPU timing)."""
+    import tempfile
+
+    cores = sorted(os.sched_getaffinity(0))
+    if not _ref_bench_available() or len(cores) <= 3:
+        return {}
+    case, prob, cfg = load_problem("cmap1_n2000")
+    work = tempfile.mkdtemp(prefix="rl_cpu_mc_")
+    try:
+        return {"reference_multicore": reference_multicore(prob, cfg, cores[2:2 + ALLCORE_CORES], work,
+                                                           int(cfg.max_outer_iters))}
+    finally:
+        import shutil
+
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def cpu_leg(budget_s: float) -> dict:
     """Everything the bench needs from the CPU, computed without touching the GPU:
     the baseline on one pinned core, the reference's per-track drop-in times, and the
@@ -226,10 +247,6 @@ def cpu_leg(budget_s: float) -> dict:
             ts = [float(np.median(O.run_ref_bench(p, c, mt, 0.0, 3, work)["ms"])) for mt in (False, True)]
             per[name] = {"N": p.N, "mincurv_ms": round(ts[0], 2), "mintime_ms": round(ts[1], 2)}
         res["reference_per_track"] = per
-    # ---- context only (SURVEY §8d optional): the reference instance-parallel on
-    # this GPU's host CPU share -- one ref_bench process per core, each pinned, on C2's problem
-    if have_ref and len(cores) > 3:
-        res["reference_multicore"] = reference_multicore(prob, cfg, cores[2:2 + ALLCORE_CORES], work, MO)
     # ---- oracle laps for the lap-Δ statistics (C3 sample, the whole C4 grid)
     c3case, _, cfg3 = load_problem("cmap1_n2000_vp20")
     c3_seeds = list(range(0, C3_BATCH, C3_BATCH // C3_SAMPLE))
@@ -301,19 +318,35 @@ def start_cpu_leg(budget_s: float):
     """The CPU leg as a child process (before the parent touches the GPU).  The parent
     then keeps to the cores the child does not use first."""
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-leg", "--cpu-budget", str(budget_s)]
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     cores = sorted(os.sched_getaffinity(0))
     if len(cores) > 1:
         os.sched_setaffinity(0, {cores[1]})
     return proc
 
 
-def finish_cpu_leg(proc):
-    out, err = proc.communicate(timeout=900)
+def read_cpu_leg(proc):
+    """The CPU leg's first line (baseline, laps, per-track reference times); None if the
+    child failed.  The child then waits for finish_cpu_leg."""
+    line = proc.stdout.readline()
+    if not line.strip():
+        finish_cpu_leg(proc, False)
+        return None
+    return json.loads(line)
+
+
+def finish_cpu_leg(proc, multicore: bool):
+    """Tell the waiting child whether to run the multicore context leg (after every GPU
+    leg), and return its result ({} when skipped or failed)."""
+    try:
+        out, err = proc.communicate(input="go\n" if multicore else "stop\n", timeout=900)
+    except (BrokenPipeError, OSError):
+        out, err = proc.communicate(timeout=900)
     if proc.returncode != 0:
         sys.stderr.write(err[-4000:])
-        return None
-    return json.loads(out.strip().splitlines()[-1])
+        return {}
+    lines = out.strip().splitlines()
+    return json.loads(lines[-1]) if lines else {}
 
 
 def lap_delta(gpu, oracle) -> dict:
@@ -364,7 +397,8 @@ def run_c4(world, rank, local, dev, dist):
     base = load_problem("track_training_map")[2]
     cfgs = D.c4_cfgs(base)
     plans, mt_plans, meta = [], [], []
-    n_flight = sum(len(ks) for ks in groups.values())     # instances of all concurrent plans
+    # instances of all concurrent plans: both modes of every group run at once
+    n_flight = 2 * sum(len(ks) for ks in groups.values())
     shapes = {}
     for t, ks in groups.items():
         case, prob, _ = load_problem("track_" + D.C4_TRACKS[t])
@@ -400,12 +434,10 @@ def run_c4(world, rank, local, dev, dist):
     for pl in plans:
         pl.close()
     if dist is not None:
-        stats = torch.tensor([[dt, float(n_inst)]], dtype=torch.float64, device=dev)
-        allst = D.gather_rows(stats, world, rank)
+        allst = D.gather_stats([dt, float(n_inst)], world, rank, device=dev)
         laps = D.gather_ragged(laps, world, rank, C4_ITEMS, device=dev)
         if rank != 0:
             return None, None
-        allst = allst.cpu().numpy()
         dt, n_inst = float(allst[:, 0].max()), int(allst[:, 1].sum())
     return {"instances": int(n_inst), "modes": "min-curv + min-time", "ms": round(dt * 1e3, 3),
             "rank0_plan_shapes_KxT": shapes, "shape_batch": n_flight,
@@ -415,13 +447,11 @@ def run_c4(world, rank, local, dev, dist):
 
 def run_c5(world, rank, local, dev, dist):
     """C5: synthetic oval N=10000 (streaming kernel, HBM-bound), 1024 seeds per rank, min-curv."""
-    import torch
-
     case, prob, cfg = load_problem("oval_n10000")
     B = 1024
-    s, _ = D.shard_range(world * B, world, rank)
-    plan = raceline.Plan(prob, cfg, seeds=np.arange(s, s + B, dtype=np.uint64), B=B,
-                         modes=abi.RL_MODE_MINCURV, device=local)
+    seeds = D.seed_block(world, rank, B)
+    s = int(seeds[0])
+    plan = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=abi.RL_MODE_MINCURV, device=local)
     plan.run()
     mc, _ = plan.fetch()
     if dist is not None:
@@ -437,11 +467,9 @@ def run_c5(world, rank, local, dev, dist):
     rel = float(np.max(np.abs(mc.x[0] - case["mc_x"])) / np.max(np.abs(case["mc_x"]))) if s == 0 else 0.0
     plan.close()
     if dist is not None:
-        st = torch.tensor([[k_ms, rel]], dtype=torch.float64, device=dev)
-        arr = D.gather_rows(st, world, rank)
+        arr = D.gather_stats([k_ms, rel], world, rank, device=dev)
         if rank != 0:
             return None
-        arr = arr.cpu().numpy()
         k_ms, rel = float(arr[:, 0].max()), float(arr[:, 1].max())
     pmc = read_pmc("c5_mincurv")
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "rl_stream_kernel<closed,mincurv>",
@@ -520,39 +548,46 @@ def run_dropin(local):
     return out
 
 
-def run_c2_pcie(prob, cfg, B, MO, rank):
+def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
     """C2 through the synchronous host-buffer entry point rl_optimize (the drop-in use):
     upload, kernel, download of all result columns into fresh numpy arrays (PCIe and the
-    host copies included).  The C side copies the results out with up to 8 host threads,
-    so this leg runs with the host cores the CPU leg leaves free."""
+    host copies included).  The download overlaps the kernel (rl_last_call_download: groups
+    of finished instances copied out while later ones compute); the C side copies the
+    results out with up to 8 host threads, so this leg runs after the CPU leg, with the
+    process's host cores."""
     import ctypes as C
 
     lib = abi.load_library()
     seeds = np.arange(rank * B, (rank + 1) * B, dtype=np.uint64)
     prev = os.sched_getaffinity(0)
-    spare = sorted(HOST_CORES)[17:25] if len(HOST_CORES) > 17 else []
-    if spare:
-        os.sched_setaffinity(0, set(spare) | prev)
+    cores = sorted(HOST_CORES)[:ALLCORE_CORES] if HOST_CORES else sorted(prev)
+    os.sched_setaffinity(0, set(cores))
     try:
         raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
         ts, ks = [], []
-        for _ in range(3):
+        for _ in range(reps):
             t0 = time.perf_counter()
             out = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
             ts.append(time.perf_counter() - t0)
             del out                  # the caller keeps its results: freeing them is not part of the call
             run, kmc, cm = C.c_float(), C.c_float(), C.c_float()
             lib.rl_last_call_times(C.byref(run), C.byref(kmc), None, C.byref(cm))
-            ks.append((run.value, kmc.value, cm.value))
+            g, sg = C.c_int32(), C.c_int32()
+            lib.rl_last_call_download(C.byref(g), C.byref(sg))
+            ks.append((run.value, kmc.value, cm.value, g.value, sg.value))
     finally:
         os.sched_setaffinity(0, prev)
     t = float(np.median(ts))
     return {"call_ms_median": round(t * 1e3, 2), "outer_iters_per_s": round(B * MO / t, 1),
-            "run_bracket_ms_median": round(float(np.median([r for r, _, _ in ks])), 3),
-            "kernel_ms_median": round(float(np.median([k for _, k, _ in ks])), 3),
-            "abi_call_ms_median": round(float(np.median([c for _, _, c in ks])), 3),
-            "host_cores": len(spare) + len(prev),
-            "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8)}
+            "call_ms_all": [round(x * 1e3, 2) for x in ts],
+            "run_bracket_ms_median": round(float(np.median([k[0] for k in ks])), 3),
+            "kernel_ms_median": round(float(np.median([k[1] for k in ks])), 3),
+            "abi_call_ms_median": round(float(np.median([k[2] for k in ks])), 3),
+            "download_groups": int(ks[-1][3]), "download_groups_signalled_min": int(min(k[4] for k in ks)),
+            "host_cores": len(cores),
+            "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8),
+            "note": "kernel_ms is the optimiser after the GPU's idle gap between calls (DESIGN §3e); the "
+                    "download of each group of 64 finished instances overlaps the later instances' compute"}
 
 
 def run_step6(world, rank):
@@ -630,6 +665,51 @@ def run_format(world, rank, mc_x, mc_y, mc_k, mc_al, case, cfg):
             "bytes_equal_on_sample": text[: len(cpu_text)] == cpu_text, "sample_rows": k}
 
 
+def run_result_gather(res_buf, res, world, rank, dev, dist, backend, same_device, B, N, MO, reps: int = 3):
+    """SURVEY §8e's final gather at its real size, outside the timed C2 steps: every rank's
+    whole min-curvature result block (x, y, κ, α_last, α_total, heading: [B][N] float64
+    each, and evals [B][MO] int32; one contiguous buffer the plan writes into) gathered to
+    rank 0 with one collective per rank -- RCCL over xGMI under the nccl backend, host
+    copies under gloo.  Timed between barriers + device syncs, `reps` times; the max over
+    ranks of the median is reported.  Rank 0 then checks block 0 against its own buffer and
+    every block's per-instance summary against the summary rows its rank sent in the timed
+    steps (bit for bit)."""
+    import torch
+
+    nbytes = int(res_buf.numel())
+    ts, blocks = [], None
+    for _ in range(reps):
+        blocks = None
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        blocks = D.gather_result_blocks(res_buf, world, rank)
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    st = D.gather_stats([float(np.median(ts)), float(min(ts))], world, rank, device=dev if backend == "nccl" else None)
+    mine = D.instance_summary(res["evals"], res["x"], res["alpha_last"]).cpu()
+    sums = D.gather_rows(mine.to(dev) if backend == "nccl" else mine, world, rank)
+    if rank != 0:
+        return None
+    sums = sums.cpu().numpy().reshape(world, B, 3)
+    ok0 = bool(torch.equal(blocks[0].to(res_buf.device), res_buf))
+    ok = []
+    for r, blk in enumerate(blocks):
+        v = D.result_views(blk.to(dev), B, N, MO)
+        ok.append(bool(np.array_equal(D.instance_summary(v["evals"], v["x"], v["alpha_last"]).cpu().numpy(), sums[r])))
+    t_med, t_min = float(st[:, 0].max()), float(st[:, 1].max())
+    where = "same-device rehearsal" if same_device else "one rank per GPU"
+    return {"bytes_per_rank": nbytes, "bytes_total": nbytes * world, "instances_gathered": world * B,
+            "arrays": list(D.RESULT_F64) + ["evals"], "reps": reps,
+            "ms": round(t_med * 1e3, 3), "ms_min": round(t_min * 1e3, 3),
+            "GBps_per_rank": round(nbytes / t_med / 1e9, 2),
+            "rank0_ingress_GBps": round(nbytes * (world - 1) / t_med / 1e9, 2),
+            "backend": ("RCCL (torch.distributed nccl gather) over xGMI, device to device" if backend == "nccl"
+                        else f"torch.distributed {backend} gather of host copies (device->host included)") + f"; {where}",
+            "rank0_block_equals_own": ok0, "blocks_equal_step_summaries": all(ok),
+            "note": "outside the timed C2 steps; max over ranks of each rank's median gather time"}
+
+
 def _free_port() -> int:
     import socket
 
@@ -670,7 +750,8 @@ def backend_label(world: int, backend: str, same_device: bool) -> str:
     coll = "RCCL (torch.distributed nccl) over xGMI" if backend == "nccl" else f"torch.distributed {backend}"
     where = (f"{world} ranks on one GPU (same-device rehearsal)" if same_device
              else f"instances sharded over {world} GPUs, one rank per GPU")
-    return f"dp{world}: {where}; per-step {coll} gather of per-instance summaries to rank 0"
+    return (f"dp{world}: {where}; per-step {coll} gather of per-instance summaries to rank 0, then one "
+            f"{coll} gather of every rank's whole result block (result_gather, outside the timed steps)")
 
 
 def main():
@@ -686,6 +767,8 @@ def main():
     args = ap.parse_args()
     if args.cpu_leg:
         print(json.dumps(cpu_leg(args.cpu_budget)), flush=True)
+        if sys.stdin.readline().strip() == "go":
+            print(json.dumps(cpu_multicore_leg()), flush=True)
         return
     cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
     if cmd is not None:
@@ -736,10 +819,9 @@ def main():
     seeds = D.seed_block(world, rank, B)
     plan = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=abi.RL_MODE_MINCURV, device=local)
 
-    # results straight into torch tensors (zero-copy for the RCCL gather)
-    f64 = dict(dtype=torch.float64, device=dev)
-    res = {k: torch.empty((B, N), **f64) for k in ("x", "y", "kappa", "alpha_last")}
-    res["evals"] = torch.empty((B, MO), dtype=torch.int32, device=dev)
+    # results straight into views of one contiguous device block per rank (zero-copy for
+    # the result gather: one RCCL collective per rank)
+    res_buf, res = D.alloc_result_block(B, N, MO, device=dev)
     plan.bind_device_outputs(abi.RL_MODE_MINCURV, {k: v.data_ptr() for k, v in res.items()})
 
     stream = torch.cuda.Stream(device=dev)
@@ -777,6 +859,8 @@ def main():
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
     total_outer = world * B * MO * args.steps
+    result_gather = run_result_gather(res_buf, res, world, rank, dev, dist, backend, same_device, B, N, MO) \
+        if world > 1 else None
     value = total_outer / elapsed
     tracks_per_s = world * B * args.steps / elapsed
 
@@ -789,8 +873,6 @@ def main():
             extras["c3_mintime_plus_mincurv"] = c3
             extras["c4_sweep_7tracks_x_512"] = c4
             extras["c5_oval_n10000"] = c5
-            extras["c2_pcie_inclusive"] = run_c2_pcie(prob, cfg, B, MO, rank)
-            extras["dropin_b1_latency"] = run_dropin(local)
             extras["open_mode_n2000"], open_gpu = run_open(local)
             extras["step6_geom_cmap1_n2000"] = run_step6(world, rank)
             xh, yh = res["x"].cpu().numpy(), res["y"].cpu().numpy()
@@ -846,6 +928,11 @@ def main():
         "frac_of_nonfma_ceiling": round(achieved_tf / FP64_NONFMA_TFLOPS, 4),
         "evals_per_outer": round(E_k, 2),
     }
+    if pmc:
+        # north_star's achieved-HBM fraction, measured: PMC bytes per launch / this kernel time
+        hbm_gbs = pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9
+        roofline["hbm_GBps_measured"] = round(hbm_gbs, 1)
+        roofline["hbm_frac_measured"] = round(hbm_gbs / HBM_PEAK_GBS, 4)
     # SURVEY §8d's streaming byte model beside the flop roofline (its achieved/8 TB/s exceeds
     # 1 at C2: the per-evaluation state lives in VGPRs/LDS and never reaches HBM)
     model_b = B * MO * bytes_per_outer(N, E_k, Eseg)
@@ -869,7 +956,16 @@ def main():
 
     cpu, cpu_res = None, None
     if cpu_proc is not None:
-        cpu_res = finish_cpu_leg(cpu_proc)
+        cpu_res = read_cpu_leg(cpu_proc)
+    # the drop-in legs (host buffers, host copy threads) once the CPU leg has left the host
+    # cores: the reference's caller has them to itself
+    if not args.no_extras:
+        extras["c2_pcie_inclusive"] = run_c2_pcie(prob, cfg, B, MO, rank)
+        extras["dropin_b1_latency"] = run_dropin(local)
+    if cpu_proc is not None:
+        mc = finish_cpu_leg(cpu_proc, cpu_res is not None)
+        if cpu_res is not None:
+            cpu_res.update(mc)
     if cpu_res is not None:
         cpu = dict(cpu_res.get("reference") or cpu_res["port"])
         cpu["cpu_model"] = cpu_res["cpu"]["model"]
@@ -923,6 +1019,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity if summary_check is None else {**parity, "gather": summary_check},
+        **({"result_gather": result_gather} if result_gather is not None else {}),
         **extras,
     }
     print(json.dumps(out), flush=True)

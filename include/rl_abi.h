@@ -170,6 +170,14 @@ int rl_last_call_ms(float* kernel_ms, float* call_ms);
  * alone from its own start and end events (-1 when that mode did not run), *call_ms = wall
  * time of the whole call.  Any pointer may be NULL. */
 int rl_last_call_times(float* run_ms, float* mincurv_ms, float* mintime_ms, float* call_ms);
+/* How the same call downloaded its results.  Calls whose results exceed 8 MiB overlap the
+ * download with the kernel: every instance signals its completion into pinned host memory,
+ * and each group of completed instances (16 per optimiser) is copied out while later
+ * instances still compute (RL_OVERLAP_DOWNLOAD=0 in the environment turns this off).
+ * *groups = the groups of the call (0: one download after the kernel), *groups_signalled =
+ * those queued on their instances' flags (the rest waited for the kernel's end).  Either
+ * pointer may be NULL.  (Not in the reference: the drop-in's own transfer path.) */
+int rl_last_call_download(int32_t* groups, int32_t* groups_signalled);
 /* Free the idle plans and pinned buffers of the cache (device memory returns to HIP). */
 int rl_release_plan_cache(void);
 /* Idle plans in the cache and the device / pinned host bytes they hold.  The cache keeps
@@ -307,8 +315,8 @@ int rl_corridor(const rl_problem* prob, const rl_cfg* cfg, int32_t device, doubl
 int         rl_device_count(void);
 const char* rl_last_error(void);
 int         rl_abi_version(void);
-/* samples per lane of the THROUGHPUT shape for N (4 or 8; 1 = the streaming kernel), or
- * RL_ETOOBIG.  Batches small enough for a latency shape launch fewer samples per lane:
+/* samples per lane of the THROUGHPUT shape for N (4: N <= 256, 5: N <= 320, 8: N <= 4096;
+ * 1 = the streaming kernel), or RL_ETOOBIG.  Batches small enough for a latency shape launch fewer samples per lane:
  * rl_kernel_shape(N, B, mode) reports the shape a launch actually uses. */
 int         rl_kernel_variant(int32_t N);
 /* the kernel shape of a launch: *K samples per lane (0 = the streaming kernel) and *T lanes

@@ -400,6 +400,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         lib.rl_last_call_times.restype = C.c_int
         lib.rl_plan_cache_info.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         lib.rl_plan_cache_info.restype = C.c_int
+    if hasattr(lib, "rl_last_call_download"):   # absent only in older experiment builds (A/B bases)
+        lib.rl_last_call_download.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.rl_last_call_download.restype = C.c_int
     if path == LIB_PATH:
         _LIB = lib
     return lib

@@ -16,6 +16,9 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include "rl_abi.h"
 #include "rl_device.h"
 #include "rl_kernels.h"
@@ -181,7 +184,7 @@ int device_cus(int dev) {
 }
 // waves of one instance in the kernel launch_optimize / launch_stream picks for (N, B, mode)
 int waves_per_instance(int N, int B, bool mintime, bool stream, int cus) {
-    if (stream) return 16;                                    // rl_stream.hip: 1024 threads
+    if (stream) return (rl::stream_threads() + 63) / 64;      // rl_stream.hip
     const rl::Shape s = rl::pick_shape(N, B, mintime, cus);
     if (s.K <= 0) return 16;
     return (s.T + 63) / 64;
@@ -218,6 +221,10 @@ struct rl_plan {
     rl_cfg* d_cfg = nullptr;
     uint64_t* d_seeds = nullptr;
     ModeBufs mb[2];
+    // per-mode instance completion flags of the next run (run_cached's overlapped
+    // download; nullptr: none) and the value the kernel stores into them
+    uint32_t* done[2] = {nullptr, nullptr};
+    uint32_t epoch = 0;
     std::vector<void*> allocs;
 
     template <class T>
@@ -264,7 +271,7 @@ int rl_kernel_shape(int32_t N, int32_t B, int32_t mode, int32_t* K, int32_t* T) 
     if (!K || !T || B < 1 || (mode != RL_MODE_MINCURV && mode != RL_MODE_MINTIME))
         return fail(RL_EINVAL, "rl_kernel_shape: bad argument");
     if (N < 1 || N > rl::RL_STREAM_MAX_N) return fail(RL_ETOOBIG, "rl_kernel_shape: N out of range");
-    if (use_stream(N)) { *K = 0; *T = 1024; return RL_OK; }   // streaming kernel (samples strided)
+    if (use_stream(N)) { *K = 0; *T = rl::stream_threads(); return RL_OK; }   // streaming kernel (samples strided)
     int dev = 0;
     const int cus = (hipGetDevice(&dev) == hipSuccess) ? device_cus(dev) : 256;
     const rl::Shape s = rl::pick_shape(N, B, mode == RL_MODE_MINTIME, cus);
@@ -345,7 +352,7 @@ int rl_plan_set_shape_batch(rl_plan* plan, int32_t shape_B) {
 int rl_plan_shape(rl_plan* plan, int32_t mode, int32_t* K, int32_t* T) {
     if (!plan || !K || !T || (mode != RL_MODE_MINCURV && mode != RL_MODE_MINTIME))
         return fail(RL_EINVAL, "rl_plan_shape: bad argument");
-    if (plan->stream) { *K = 0; *T = 1024; return RL_OK; }
+    if (plan->stream) { *K = 0; *T = rl::stream_threads(); return RL_OK; }
     const rl::Shape s = rl::pick_shape(std::max(plan->N, 1), plan->shape_B > 0 ? plan->shape_B : plan->B,
                                        mode == RL_MODE_MINTIME, device_cus(plan->device));
     *K = s.K;
@@ -574,6 +581,8 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
         kp.shape_B = sB;
         kp.L = p->L; kp.veh_width = p->veh_width;
+        kp.done = p->done[m];
+        kp.epoch = p->epoch;
         HIPCHK(hipEventRecord(p->ev[1 + m], st));
         hipError_t e = p->stream ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
@@ -960,7 +969,7 @@ size_t cache_budget() {
     if (end == s) return kCacheBytesDefault;
     return (size_t)mb << 20;
 }
-constexpr int kJobEvents = 32;
+constexpr int kJobEvents = 256;   // download events of an entry (download_staged, download_overlapped)
 
 struct CacheEntry {
     rl_plan* p = nullptr;
@@ -970,6 +979,12 @@ struct CacheEntry {
     unsigned char* pin = nullptr;                      // pinned staging
     size_t pin_bytes = 0;
     hipEvent_t ev[kJobEvents] = {};
+    // overlapped download (download_overlapped): per-mode instance completion flags in
+    // coherent pinned memory, the epoch of the last run, and the copy stream
+    uint32_t* flags = nullptr;
+    int flags_n = 0;
+    uint32_t epoch = 0;
+    hipStream_t dl = nullptr;
     uint64_t tick = 0;
 
     bool same(const CacheEntry& k) const {
@@ -979,7 +994,7 @@ struct CacheEntry {
                (segs.empty() || std::memcmp(segs.data(), k.segs.data(), segs.size() * sizeof(double)) == 0);
     }
     // device memory of the plan plus the pinned staging buffer (both stay allocated while idle)
-    size_t bytes() const { return (p ? p->dev_bytes : 0) + pin_bytes; }
+    size_t bytes() const { return (p ? p->dev_bytes : 0) + pin_bytes + (size_t)flags_n * sizeof(uint32_t); }
 };
 
 void destroy_entry(CacheEntry* e) {
@@ -990,6 +1005,11 @@ void destroy_entry(CacheEntry* e) {
     }
     for (hipEvent_t& v : e->ev)
         if (v) hipEventDestroy(v);
+    if (e->dl) {
+        hipStreamSynchronize(e->dl);
+        hipStreamDestroy(e->dl);
+    }
+    if (e->flags) hipHostFree(e->flags);
     if (e->pin) hipHostFree(e->pin);
     delete e;
 }
@@ -1059,6 +1079,7 @@ PlanCache& plan_cache() {
 
 thread_local float g_last_kernel_ms = -1.0f, g_last_call_ms = -1.0f;
 thread_local float g_last_mode_ms[2] = {-1.0f, -1.0f};    // min-curv / min-time kernel of the last call
+thread_local int g_last_groups = 0, g_last_groups_signalled = 0;   // the last call's download groups
 
 int ensure_pinned(CacheEntry* e, size_t bytes) {
     if (bytes <= e->pin_bytes) return RL_OK;
@@ -1134,12 +1155,220 @@ size_t staged_bytes(const std::vector<CopyJob>& jobs) {
     return t;
 }
 
+// ---- overlapped download (large batches)
+// The kernel of an rl_optimize call finishes its instances over its whole run (a batch of
+// B instances takes B / (instances resident) rounds), but a download that waits for the
+// kernel moves all of their results after it (C2: 98 MB, 40 % of the call).
+// Here every instance signals its completion (KParams::done, signal_done in rl_kernels.h)
+// into coherent pinned memory; the calling thread watches the flags and, as soon as every
+// instance of a group has signalled, queues that group's result slices (instance-major
+// arrays: one contiguous slice per array) on a copy stream, while the kernel still computes
+// later instances.  Helper threads copy each group out of the pinned staging as its copies
+// land.  The launch is the one rl_plan_run makes anyway, so the results are those of the
+// plan path bit for bit.  A kernel that ends without signalling some instance (or any HIP
+// failure) takes the stream-ordered path for the rest: the copy stream waits for the
+// kernel's end event.  RL_OVERLAP_DOWNLOAD=0 turns the overlap off (A/B, tests).
+constexpr size_t kOverlapMinBytes = (size_t)8 << 20;  // smaller downloads: one staged pass
+constexpr int kGroupsPerMode = 16;                     // groups of a mode
+static_assert(2 * kGroupsPerMode <= kJobEvents, "one download event per group");
+
+bool overlap_enabled() {
+    const char* s = std::getenv("RL_OVERLAP_DOWNLOAD");
+    return !(s && s[0] == '0');
+}
+
+int ensure_flags(CacheEntry* e, int B) {
+    if (!e->dl && hipStreamCreateWithFlags(&e->dl, hipStreamNonBlocking) != hipSuccess) {
+        e->dl = nullptr;
+        return fail(RL_EHIP, "hipStreamCreate (download stream) failed");
+    }
+    if (e->flags && e->flags_n >= 2 * B) return RL_OK;
+    if (e->flags) hipHostFree(e->flags);
+    e->flags = nullptr;
+    e->flags_n = 0;
+    if (hipHostMalloc((void**)&e->flags, (size_t)2 * B * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) !=
+        hipSuccess) {
+        e->flags = nullptr;
+        return fail(RL_ENOMEM, "hipHostMalloc (completion flags) failed");
+    }
+    std::memset(e->flags, 0, (size_t)2 * B * sizeof(uint32_t));
+    e->flags_n = 2 * B;
+    e->epoch = 0;
+    return RL_OK;
+}
+
+// Ask the kernel for writable pages behind [p, p + n) now (MADV_POPULATE_WRITE, Linux 5.14;
+// errors ignored): a page already present is left as it is, so this never changes the
+// caller's data and may run while another thread copies into the same range.  Fresh output
+// arrays (the reference's own use) would otherwise take their page faults inside the copies
+// after the kernel.
+void populate_write(void* p, size_t n) {
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+    static const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = (uintptr_t)p & ~(pg - 1), b = ((uintptr_t)p + n + pg - 1) & ~(pg - 1);
+    if (n) (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+}
+
+// jm[m]: mode m's download jobs (out_jobs order, every array instance-major over the plan's B
+// instances).  Called after rl_plan_run queued the kernels with p->done set.
+int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&jm)[2], uint32_t epoch) {
+    const int B = p->B;
+    const int G = std::min(kGroupsPerMode, B);
+    struct Group {
+        int m, b0, b1;
+        int s0, s1;                                    // its slices [s0, s1)
+    };
+    struct Slice {
+        void* pin;
+        const void* src;
+        size_t bytes;
+        int ev;                                        // event recorded after its copy
+    };
+    struct Piece {
+        unsigned char* dst;
+        const unsigned char* src;
+        size_t bytes;
+        int slice;
+    };
+    std::vector<Group> groups;
+    for (int m = 0; m < 2; ++m)
+        if (!jm[m].empty())
+            for (int g = 0; g < G; ++g)
+                groups.push_back({m, (int)((int64_t)B * g / G), (int)((int64_t)B * (g + 1) / G), 0, 0});
+    // staging offsets: array-major, as download_staged lays them out
+    std::vector<size_t> job_off[2];
+    size_t off = 0;
+    for (int m = 0; m < 2; ++m)
+        for (const CopyJob& j : jm[m]) {
+            job_off[m].push_back(off);
+            off += (j.bytes + 255) & ~(size_t)255;
+        }
+    // slices in publication order (group-major); one event per slice while they fit, else
+    // one per group (the group's last slice)
+    std::vector<Slice> slices;
+    std::vector<Piece> pieces;
+    const size_t kPiece = (size_t)1 << 20;
+    for (Group& g : groups) {
+        g.s0 = (int)slices.size();
+        for (size_t k = 0; k < jm[g.m].size(); ++k) {
+            const CopyJob& j = jm[g.m][k];
+            const size_t row = j.bytes / (size_t)B;    // bytes of one instance
+            const size_t o = (size_t)g.b0 * row, n = (size_t)(g.b1 - g.b0) * row;
+            if (!n) continue;
+            const int si = (int)slices.size();
+            slices.push_back({e->pin + job_off[g.m][k] + o, (const unsigned char*)j.src + o, n, -1});
+            for (size_t q = 0; q < n; q += kPiece)
+                pieces.push_back({(unsigned char*)j.dst + o + q, e->pin + job_off[g.m][k] + o + q, std::min(kPiece, n - q), si});
+        }
+        g.s1 = (int)slices.size();
+    }
+    const bool per_slice = slices.size() <= (size_t)kJobEvents;
+    for (size_t gi = 0; gi < groups.size(); ++gi)
+        for (int si = groups[gi].s0; si < groups[gi].s1; ++si) slices[si].ev = per_slice ? si : (int)gi;
+    std::atomic<size_t> next{0}, next_pop{0};
+    std::atomic<int> published{0};                     // slices queued (publication order)
+    std::atomic<bool> bad{false};
+    auto work = [&](bool populate) {
+        if (populate)                                  // while the first instances still compute
+            for (size_t i; (i = next_pop.fetch_add(1)) < jm[0].size() + jm[1].size();) {
+                const CopyJob& j = i < jm[0].size() ? jm[0][i] : jm[1][i - jm[0].size()];
+                populate_write(j.dst, j.bytes);
+            }
+        for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+            const int si = pieces[i].slice;
+            while (published.load(std::memory_order_acquire) <= si) {
+                if (bad.load()) return;
+                std::this_thread::sleep_for(std::chrono::microseconds(10));
+            }
+            if (hipEventSynchronize(e->ev[slices[si].ev]) != hipSuccess) {
+                bad = true;
+                return;
+            }
+            std::memcpy(pieces[i].dst, pieces[i].src, pieces[i].bytes);
+        }
+    };
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nthr = (int)std::min<size_t>({8, hw, pieces.size() + 1});
+    std::vector<std::thread> th;
+    try {
+        th.reserve((size_t)std::max(0, nthr - 1));
+        for (int t = 1; t < nthr; ++t) th.emplace_back(work, true);
+    } catch (...) {
+    }
+    // the calling thread watches the flags and queues each finished group's copies
+    const volatile uint32_t* fl = e->flags;
+    bool joined[2] = {false, false};
+    int signalled = 0;
+#ifdef RL_OVL_TRACE     // diagnostic builds: when each group was queued, and the kernel's end
+    const auto tr0 = std::chrono::steady_clock::now();
+    auto tr_ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(); };
+    std::vector<double> tr_pub(groups.size(), -1.0);
+    double tr_end = -1.0;
+#endif
+    for (size_t gi = 0; gi < groups.size() && !bad.load(); ++gi) {
+        const Group& g = groups[gi];
+        for (int b = g.b0;;) {
+            while (b < g.b1 && fl[(size_t)g.m * B + b] == epoch) ++b;
+            if (b == g.b1) break;
+            if (joined[g.m]) break;
+            const hipError_t q = hipEventQuery(p->ev_end[g.m]);
+            if (q == hipSuccess) {
+                // the kernel has ended without this flag: stream order from here on
+                if (hipStreamWaitEvent(e->dl, p->ev_end[g.m], 0) != hipSuccess) bad = true;
+                joined[g.m] = true;
+                break;
+            }
+            if (q != hipErrorNotReady) {
+                bad = true;
+                break;
+            }
+            std::this_thread::yield();
+        }
+        if (bad.load()) break;
+        for (int si = g.s0; si < g.s1 && !bad.load(); ++si) {
+            const Slice& sl = slices[si];
+            if (hipMemcpyAsync(sl.pin, sl.src, sl.bytes, hipMemcpyDeviceToHost, e->dl) != hipSuccess ||
+                (per_slice && hipEventRecord(e->ev[sl.ev], e->dl) != hipSuccess))
+                bad = true;
+        }
+        if (!per_slice && !bad.load() && hipEventRecord(e->ev[gi], e->dl) != hipSuccess) bad = true;
+        if (bad.load()) break;
+        published.store(g.s1, std::memory_order_release);
+        if (!joined[g.m]) ++signalled;
+#ifdef RL_OVL_TRACE
+        tr_pub[gi] = tr_ms();
+#endif
+    }
+#ifdef RL_OVL_TRACE
+    if (hipEventSynchronize(p->ev_end[groups.back().m]) == hipSuccess) tr_end = tr_ms();
+#endif
+    work(false);
+    for (auto& t : th) t.join();
+#ifdef RL_OVL_TRACE
+    {
+        const double tr_copy = tr_ms();
+        hipStreamSynchronize(e->dl);
+        std::fprintf(stderr, "{\"ovl_trace\": {\"kernel_end_seen_ms\": %.3f, \"copies_done_ms\": %.3f, \"published_ms\": [", tr_end, tr_copy);
+        for (size_t i = 0; i < tr_pub.size(); ++i) std::fprintf(stderr, "%s%.3f", i ? ", " : "", tr_pub[i]);
+        std::fprintf(stderr, "]}}\n");
+    }
+#endif
+    const bool synced = hipStreamSynchronize(e->dl) == hipSuccess;
+    if (bad.load() || !synced) return fail(RL_EHIP, "download (overlapped) failed");
+    g_last_groups = (int)groups.size();
+    g_last_groups_signalled = signalled;
+    return RL_OK;
+}
+
 // rl_optimize / rl_lap_eval through the plan cache (see above).  kms[0..2]: HIP-event
 // times of the whole run, the min-curvature and the min-time kernel (-1 if not run).
 int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
                int32_t modes, const double* centers, const double* Ls, rl_out* out_mc, rl_out* out_mt, float* kms) {
     const auto t0 = std::chrono::steady_clock::now();
     g_last_kernel_ms = g_last_call_ms = g_last_mode_ms[0] = g_last_mode_ms[1] = -1.0f;
+    g_last_groups = g_last_groups_signalled = 0;
     if (int rc = check_inputs(prob, cfg, n_cfg, B, modes, centers)) return rc;
     int ndev = 0, dev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RL_ENODEV, "no HIP device");
@@ -1205,18 +1434,39 @@ int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const u
     }
     rl_plan* p = e->p;
     p->modes = modes;
-    std::vector<CopyJob> jobs;
-    out_jobs(p, 0, (modes & RL_MODE_MINCURV) ? out_mc : nullptr, jobs);
-    out_jobs(p, 1, (modes & RL_MODE_MINTIME) ? out_mt : nullptr, jobs);
-    // the staging area serves the uploads first, then (stream-ordered after the kernel)
-    // the downloads; a reallocation waits for the uploads already queued
+    std::vector<CopyJob> jm[2], jobs;
+    out_jobs(p, 0, (modes & RL_MODE_MINCURV) ? out_mc : nullptr, jm[0]);
+    out_jobs(p, 1, (modes & RL_MODE_MINTIME) ? out_mt : nullptr, jm[1]);
+    jobs = jm[0];
+    jobs.insert(jobs.end(), jm[1].begin(), jm[1].end());
+    // the staging area serves the uploads first, then (after the kernel has started, or
+    // stream-ordered after it) the downloads; a reallocation waits for the uploads queued
     const size_t down_bytes = staged_bytes(jobs);
     if (down_bytes > e->pin_bytes) {
         if (hipStreamSynchronize(p->own_stream) != hipSuccess) return drop(fail(RL_EHIP, "upload sync"));
         if ((rc = ensure_pinned(e, down_bytes))) return drop(rc);
     }
-    if ((rc = rl_plan_run(p, nullptr))) return drop(rc);
-    if ((rc = download_staged(e, p->own_stream, jobs, 0))) return drop(rc);
+    const bool overlap = overlap_enabled() && p->N > 0 && B >= 2 && down_bytes >= kOverlapMinBytes;
+    uint32_t epoch = 0;
+    if (overlap) {
+        if ((rc = ensure_flags(e, B))) return drop(rc);
+        uint32_t* dflags = nullptr;
+        if (hipHostGetDevicePointer((void**)&dflags, e->flags, 0) != hipSuccess || !dflags)
+            return drop(fail(RL_EHIP, "hipHostGetDevicePointer (completion flags) failed"));
+        if (++e->epoch == 0) {                         // wrapped: no flag may hold the new epoch
+            std::memset(e->flags, 0, (size_t)e->flags_n * sizeof(uint32_t));
+            e->epoch = 1;
+        }
+        epoch = e->epoch;
+        p->epoch = epoch;
+        for (int m = 0; m < 2; ++m) p->done[m] = jm[m].empty() ? nullptr : dflags + (size_t)m * B;
+    }
+    rc = rl_plan_run(p, nullptr);
+    p->done[0] = p->done[1] = nullptr;                 // later runs of this plan signal nothing
+    if (rc) return drop(rc);
+    if (overlap) rc = download_overlapped(e, p, jm, epoch);
+    else rc = download_staged(e, p->own_stream, jobs, 0);
+    if (rc) return drop(rc);
     if (hipStreamSynchronize(p->own_stream) != hipSuccess) return drop(fail(RL_EHIP, "stream sync"));
     float ms[3] = {-1.0f, -1.0f, -1.0f};
     for (int i = 0; i < 3; ++i) {
@@ -1256,6 +1506,13 @@ int rl_last_call_times(float* run_ms, float* mincurv_ms, float* mintime_ms, floa
     if (mincurv_ms) *mincurv_ms = g_last_mode_ms[0];
     if (mintime_ms) *mintime_ms = g_last_mode_ms[1];
     if (call_ms) *call_ms = g_last_call_ms;
+    return RL_OK;
+}
+
+int rl_last_call_download(int32_t* groups, int32_t* groups_signalled) {
+    if (g_last_call_ms < 0.0f) return fail(RL_EINVAL, "no successful rl_optimize / rl_lap_eval on this thread");
+    if (groups) *groups = g_last_groups;
+    if (groups_signalled) *groups_signalled = g_last_groups_signalled;
     return RL_OK;
 }
 

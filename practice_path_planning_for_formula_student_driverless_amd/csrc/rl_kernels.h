@@ -26,7 +26,22 @@ struct KParams {
     int32_t shape_B;           // batch size the kernel shape is chosen for (pick_shape; >= 1)
     int64_t center_stride;     // doubles between instances' centres (0: shared)
     double L, veh_width;
+    // Instance completion flags (rl_optimize's overlapped download, rl_abi.cpp run_cached):
+    // nullptr, or [B] words in coherent pinned host memory; instance b stores `epoch` into
+    // done[b] once every result word of b has reached memory (signal_done below)
+    uint32_t* done;
+    uint32_t epoch;
 };
+
+// The instance's completion flag: every thread's result stores are written back to memory
+// (a system-scope release fence: the L2 write-back, then the wait for it), the workgroup
+// joins, then one lane stores the epoch into the host-visible flag with a vector store.
+// Called once, at the very end of the kernel, uniformly by every thread of the workgroup.
+__device__ __forceinline__ void signal_done(uint32_t* done, int b, uint32_t epoch) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Per-instance HBM state of the large-N streaming kernel (rl_stream.hip): RL_STREAM_ARRAYS
 // arrays of N doubles per instance, instance-major [B][RL_STREAM_ARRAYS][N] in one allocation
@@ -39,7 +54,7 @@ constexpr int RL_STREAM_ARRAYS = 15;
 constexpr int RL_REG_MAX_N = 4096;          // register-resident kernel covers N <= 4096
 constexpr int RL_STREAM_MAX_N = 1 << 20;
 
-// samples per lane for N (4 or 8) of the throughput shapes, or -1 if N exceeds the
+// samples per lane for N (4, 5 or 8) of the throughput shapes, or -1 if N exceeds the
 // register-resident kernel
 int pick_k(int N);
 // (K samples per lane, T lanes per instance) of a register-resident launch
@@ -85,8 +100,10 @@ hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
 hipError_t launch_optimize_lat(const KParams& p, bool mintime, hipStream_t st);
 // the (4, 512) launches (1024 < N <= 2048), rl_kernels_mid.hip
 hipError_t launch_optimize_mid(const KParams& p, bool mintime, hipStream_t st);
-// large-N variant: one 1024-thread workgroup per instance, state in HBM
+// large-N variant: one workgroup of stream_threads() threads per instance, state in HBM
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st);
+// threads per instance of the streaming kernel (its build knob RL_STS, 1024 by default)
+int stream_threads();
 // step 6 geometry (rl_geom.hip): spline knots [5][nk] per axis (s,a,b,c,d), rows [Kmax+dup][9]
 struct GeomParams {
     const double* kx;

@@ -1655,6 +1655,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
         RL_STAMP(4);
     }
+    if (p.done) signal_done(p.done, b, p.epoch);
 #ifdef RL_STAMPS
     RL_STAMP(6);
     if (tid == 0 && b < 16384) {

@@ -1022,6 +1022,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
         }
         RL_SSTAMP(4);
     }
+    if (p.done) signal_done(p.done, b, p.epoch);
 #ifdef RL_STAMPS
     if (tid == 0 && b < 16384) {
         for (int i = 0; i < 16; ++i) rl_dbg_stamps_s[b][i] = st_acc[i];
@@ -1052,6 +1053,8 @@ static hipError_t launch_s(const KParams& p, const StreamBufs& sb, hipStream_t s
 }
 
 #undef PPT
+
+int stream_threads() { return TS; }
 
 hipError_t launch_stream(const KParams& p, const StreamBufs& sb, bool mintime, hipStream_t st) {
     if (p.N <= 0 || p.N > RL_STREAM_MAX_N) return hipErrorInvalidValue;

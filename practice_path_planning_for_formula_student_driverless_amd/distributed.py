@@ -53,8 +53,9 @@ def seed_block(world: int, rank: int, B: int) -> np.ndarray:
 
 def instance_summary(evals, x, alpha_last):
     """Per-instance summary rows [B, 3] = (Σ evaluations, Σ x, Σ α_last): what every rank
-    sends to rank 0 each step (a gather of per-instance summaries; the full
-    SoA results stay resident on each rank).  torch tensors in, float64 tensor out."""
+    sends to rank 0 each step (a gather of per-instance summaries); the full
+    SoA results are gathered once after the timed steps (gather_result_blocks).  torch
+    tensors in, float64 tensor out."""
     import torch
 
     return torch.stack([evals.sum(1, dtype=torch.float64), x.sum(1), alpha_last.sum(1)], dim=1)
@@ -67,6 +68,64 @@ def gather_rows(t, world: int, rank: int, group=None):
 
     got = gather_to_root({"t": t}, world, rank, group)
     return torch.cat(got["t"]) if rank == 0 else None
+
+
+def gather_stats(values: Sequence[float], world: int, rank: int, device=None, group=None):
+    """Gather one row of float64 values per rank to rank 0: a numpy [world, len(values)]
+    array on rank 0 (row r = rank r's values), None elsewhere.  The bench reduces the rows
+    (max of the per-rank times, sum of the instance counts)."""
+    import torch
+
+    t = torch.tensor([list(values)], dtype=torch.float64, device=device)
+    rows = gather_rows(t, world, rank, group)
+    return rows.cpu().numpy() if rank == 0 else None
+
+
+# --------------------------------------------------------- result block (SURVEY §8e gather)
+# One rank's min-curvature results as ONE contiguous byte buffer, so the final gather is a
+# single collective per rank: six [B][N] float64 columns, then the [B][MO] int32
+# evaluations.  The plan writes its outputs straight into views of the buffer
+# (rl_plan_bind_device_outputs), so gathering needs no packing copy.
+RESULT_F64 = ("x", "y", "kappa", "alpha_last", "alpha_total", "heading")
+
+
+def result_layout(B: int, N: int, MO: int) -> Dict[str, Tuple[int, int, str, Tuple[int, int]]]:
+    """{name: (byte offset, bytes, dtype name, shape)} of a result block."""
+    out, off = {}, 0
+    for name in RESULT_F64:
+        n = B * N * 8
+        out[name] = (off, n, "float64", (B, N))
+        off += n
+    out["evals"] = (off, B * MO * 4, "int32", (B, MO))
+    return out
+
+
+def result_block_bytes(B: int, N: int, MO: int) -> int:
+    return sum(v[1] for v in result_layout(B, N, MO).values())
+
+
+def result_views(buf, B: int, N: int, MO: int) -> Dict[str, "object"]:
+    """Typed views (torch) of a uint8 result block: {name: tensor of its dtype and shape}."""
+    import torch
+
+    dt = {"float64": torch.float64, "int32": torch.int32}
+    return {name: buf[o:o + n].view(dt[d]).view(*shape) for name, (o, n, d, shape) in result_layout(B, N, MO).items()}
+
+
+def alloc_result_block(B: int, N: int, MO: int, device=None):
+    """A zeroed uint8 result block on `device` and its typed views."""
+    import torch
+
+    buf = torch.zeros(result_block_bytes(B, N, MO), dtype=torch.uint8, device=device)
+    return buf, result_views(buf, B, N, MO)
+
+
+def gather_result_blocks(buf, world: int, rank: int, group=None):
+    """dist.gather of every rank's result block to rank 0 (RCCL over xGMI with the nccl
+    backend, device to device; gloo gathers host copies).  Returns the list of blocks in
+    rank order on rank 0, None elsewhere."""
+    got = gather_to_root({"r": buf}, world, rank, group)
+    return got["r"] if rank == 0 else None
 
 
 def gather_ragged(a: np.ndarray, world: int, rank: int, total: int, device=None, group=None):

@@ -16,6 +16,8 @@ for p in sorted(glob.glob(os.path.join(REPO, "practice_path_planning_for_formula
         libs[n] = abi.load_library(p)
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 CASES = ["track_training_map", "track_competition_map1", "track_competition_map_testday3", "cmap1_n2000"]
+if os.environ.get("AB_LAT_CASES"):
+    CASES = os.environ["AB_LAT_CASES"].split(",")
 res = {}
 for cname in CASES:
     case = O.load_case(cname); prob = O.case_problem(case); cfg = O.case_cfg(case)

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Ground truth for scripts/corridor_sim_sorted.py: the streaming kernel's corridor counters
+(RL_COUNT diagnostic build, _lib/variants/librl_count.so) on C5's problem for jittered seeds
+1..16, with max_outer_iters = 1 (one corridor pass: the centre line's), 2 and 14 (a pass
+per outer iteration), so the visited fraction of ray blocks splits into the first pass and
+the later ones (on the path the seeded first outer iteration left)."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import oracle_lib as O  # noqa: E402
+from practice_path_planning_for_formula_student_driverless_amd import abi  # noqa: E402
+
+lib = abi.load_library(os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_amd/_lib/variants/librl_count.so"))
+case = O.load_case("oval_n10000")
+prob, cfg0 = O.case_problem(case), O.case_cfg(case)
+B = 16
+seeds = np.arange(1, B + 1, dtype=np.uint64)
+out = {}
+for mo in (1, 2, 14):
+    cfg = abi.RlCfg.from_dict(cfg0.to_dict())
+    cfg.max_outer_iters = mo
+    h = C.c_void_p()
+    p = prob.as_c()
+    arr, n = abi.cfg_array(cfg)
+    assert lib.rl_plan_create(C.byref(h), 0, C.byref(p), arr, n, abi.u64ptr(seeds), B, 1) == 0
+    cnt = np.zeros(8, dtype=np.uint64)
+    lib.rl_debug_counts(cnt.ctypes.data_as(C.c_void_p), 1)
+    assert lib.rl_plan_run(h, None) == 0
+    o = abi.Outputs.alloc(B, prob.N, max(mo, 1), False)
+    oc = o.as_c()
+    assert lib.rl_plan_fetch(h, C.byref(oc), None) == 0
+    lib.rl_debug_counts(cnt.ctypes.data_as(C.c_void_p), 0)
+    lib.rl_plan_destroy(h)
+    out[mo] = [int(v) for v in cnt]
+    print(json.dumps({"max_outer": mo, "ray_blocks": out[mo][0], "ray_blocks_visited": out[mo][1],
+                      "visited_fraction": round(out[mo][1] / max(1, out[mo][0]), 4),
+                      "evals_outer0": o.evals[:, 0].tolist()[:4] if mo else None}), flush=True)
+# the later passes alone (max_outer 14 minus the one pass of max_outer 1)
+later = (out[14][1] - out[1][1]) / max(1, out[14][0] - out[1][0])
+print(json.dumps({"first_pass_visited": round(out[1][1] / max(1, out[1][0]), 4), "later_passes_visited": round(later, 4)}),
+      flush=True)

@@ -35,7 +35,7 @@ def test_header_declares_expected_entry_points():
                  "rl_plan_device_outputs", "rl_plan_kernel_ms", "rl_plan_bind_device_outputs", "rl_cfg_default", "rl_cfg_set_mu",
                  "rl_ring_segments", "rl_seed_value", "rl_device_count", "rl_last_error", "rl_abi_version",
                  "rl_kernel_variant", "rl_geom", "rl_optimize_multi", "rl_lap_eval", "rl_corridor", "rl_format_csv",
-                 "rl_last_call_ms", "rl_last_call_times", "rl_release_plan_cache", "rl_plan_cache_info",
+                 "rl_last_call_ms", "rl_last_call_times", "rl_last_call_download", "rl_release_plan_cache", "rl_plan_cache_info",
                  "rl_kernel_shape", "rl_plan_set_shape_batch", "rl_plan_shape"):
         assert must in names
 
@@ -111,6 +111,11 @@ def test_seed_values_equal_oracle():
 def test_kernel_variant_table():
     lib = abi.load_library()
     assert lib.rl_kernel_variant(187) == 4
+    assert lib.rl_kernel_variant(256) == 4
+    assert lib.rl_kernel_variant(257) == 5           # (5, 64): testday1/3 (N = 259/261)
+    assert lib.rl_kernel_variant(300) == 5
+    assert lib.rl_kernel_variant(320) == 5
+    assert lib.rl_kernel_variant(321) == 8
     assert lib.rl_kernel_variant(2000) == 8
     assert lib.rl_kernel_variant(4096) == 8
     assert lib.rl_kernel_variant(4097) == 1          # large-N streaming kernel
@@ -155,6 +160,8 @@ def test_plan_cache_queries_without_a_call():
         assert (n.value, d.value, h.value) == (0, 0, 0)
         f = C.c_float()
         assert lib.rl_last_call_times(C.byref(f), None, None, None) == abi.RL_EINVAL
+        g = C.c_int32()
+        assert lib.rl_last_call_download(C.byref(g), None) == abi.RL_EINVAL
 
 
 def test_compute_fails_loudly_without_gpu():

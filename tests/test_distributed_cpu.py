@@ -80,6 +80,22 @@ def _c4_shard_laps(world, rank):
     return np.array(laps)
 
 
+def _c2_result_block(seeds):
+    """The bench's per-rank result block (distributed.alloc_result_block: x, y, κ, α_last,
+    α_total, heading, evals in one byte buffer) filled by the CPU oracle: training_map,
+    2 outer iterations, the given seeds."""
+    import oracle_lib as O
+
+    case = O.load_case("track_training_map")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    cfg.max_outer_iters = 2
+    mc, _ = O.run_oracle(prob, cfg, seeds=seeds, B=len(seeds), modes=(True, False))
+    buf, v = D.alloc_result_block(len(seeds), prob.N, 2)
+    for name in D.RESULT_F64 + ("evals",):
+        v[name].copy_(torch.from_numpy(np.ascontiguousarray(getattr(mc, name))))
+    return buf
+
+
 def _bench_path_worker(rank, world, port, q):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -91,24 +107,27 @@ def _bench_path_worker(rank, world, port, q):
     rows = D.gather_rows(summary, world, rank)
     n_items = C4_SMALL["n_tracks"] * C4_SMALL["n_points"]
     laps = D.gather_ragged(_c4_shard_laps(world, rank), world, rank, n_items)
+    blocks = D.gather_result_blocks(_c2_result_block(D.seed_block(world, rank, B)), world, rank)
     if rank == 0:
-        q.put((rows.numpy(), laps))
+        q.put((rows.numpy(), laps, [b.numpy() for b in blocks]))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_path_gather_equals_one_rank(world):
-    """world-size 2/3 over gloo: per-rank seed blocks, the per-step summary gather and the
-    track-major C4 lap gather (the functions bench.py runs over RCCL), each rank computing
-    its shard with the CPU oracle; rank 0's gathered rows equal a one-rank run."""
+    """world-size 2/3 over gloo: per-rank seed blocks, the per-step summary gather, the
+    track-major C4 lap gather and the final result-block gather (the functions bench.py
+    runs over RCCL), each rank computing its shard with the CPU oracle; rank 0's gathered
+    rows equal a one-rank run, and its gathered block r equals rank r's own block bit for
+    bit (every column of the SoA, evaluations included)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_bench_path_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    rows, laps = q.get(timeout=300)
+    rows, laps, blocks = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -116,6 +135,109 @@ def test_bench_path_gather_equals_one_rank(world):
     np.testing.assert_array_equal(rows, one)
     np.testing.assert_array_equal(laps, _c4_shard_laps(1, 0))
     assert rows.shape == (2 * world, 3) and len(laps) == C4_SMALL["n_tracks"] * C4_SMALL["n_points"]
+    assert len(blocks) == world
+    for r, blk in enumerate(blocks):
+        own = _c2_result_block(D.seed_block(world, r, 2)).numpy()
+        assert blk.dtype == np.uint8 and blk.shape == own.shape
+        np.testing.assert_array_equal(blk, own)
+        # the block's views read back the rank's oracle columns
+        v = D.result_views(torch.from_numpy(blk), 2, _training_n(), 2)
+        s = D.instance_summary(v["evals"], v["x"], v["alpha_last"]).numpy()
+        np.testing.assert_array_equal(s, one[2 * r:2 * r + 2])
+
+
+def _training_n():
+    import oracle_lib as O
+
+    return O.case_problem(O.load_case("track_training_map")).N
+
+
+def test_result_layout():
+    """The result block: six float64 [B][N] columns then the int32 [B][MO] evaluations,
+    contiguous, views aliasing the one buffer."""
+    B, N, MO = 3, 5, 4
+    lay = D.result_layout(B, N, MO)
+    assert list(lay) == list(D.RESULT_F64) + ["evals"]
+    assert D.result_block_bytes(B, N, MO) == 6 * B * N * 8 + B * MO * 4
+    off = 0
+    for name, (o, n, _, _) in lay.items():
+        assert o == off
+        off += n
+    buf, v = D.alloc_result_block(B, N, MO)
+    v["heading"][2, 4] = 1.5
+    v["evals"][1, 3] = 7
+    o = lay["heading"][0] + (2 * N + 4) * 8
+    assert buf[o:o + 8].view(torch.float64).item() == 1.5
+    o = lay["evals"][0] + (1 * MO + 3) * 4
+    assert buf[o:o + 4].view(torch.int32).item() == 7
+
+
+def _lap_value(t, k):
+    return 1000.0 * t + k + 0.25
+
+
+def _world8_worker(rank, world, port, q):
+    """One rank of the bench's 8-GPU shard arithmetic at the bench's real sizes, with
+    synthetic per-item values in place of the GPU results."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    # C4 (run_c4): track-major groups, laps in plan order, gathered to rank 0 in item order;
+    # time = max over ranks, instances = sum
+    groups = D.c4_shard(world, rank)
+    laps = np.array([_lap_value(t, k) for t, ks in groups.items() for k in ks])
+    n_inst = sum(len(ks) for ks in groups.values())
+    out["c4_laps"] = D.gather_ragged(laps, world, rank, bench.C4_ITEMS)
+    out["c4_stats"] = D.gather_stats([1.0 + 0.1 * rank, float(n_inst)], world, rank)
+    # C5 (run_c5) and C2: 1024 seeds per rank
+    seeds = D.seed_block(world, rank, 1024)
+    out["c5_seeds"] = D.gather_rows(torch.from_numpy(seeds.astype(np.float64)).view(-1, 1), world, rank)
+    out["c5_stats"] = D.gather_stats([25.0 + rank, 0.0], world, rank)
+    # the result block (small N here; the real one is 98 MB per rank)
+    buf, v = D.alloc_result_block(4, 3, 2)
+    v["x"].fill_(float(rank))
+    v["evals"].fill_(rank + 1)
+    out["blocks"] = D.gather_result_blocks(buf, world, rank)
+    if rank == 0:
+        q.put({k: (val.numpy() if hasattr(val, "numpy") else
+                   [b.numpy() for b in val] if isinstance(val, list) else val) for k, val in out.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_world8_shard_math_at_bench_sizes():
+    """world 8 over gloo: the bench's C4 sharding of 3 584 (track, sweep
+    point) items, C2/C5's 8 x 1 024 seed blocks, the max-over-ranks time and instance-count
+    reductions, and the result-block gather -- every item exactly once, rank 0's gathered
+    order equal to the item order, the reductions equal to the per-rank values'."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world8_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    items = D.c4_items()
+    assert len(items) == 3584
+    np.testing.assert_array_equal(got["c4_laps"], [_lap_value(t, k) for t, k in items])
+    st = got["c4_stats"]
+    assert st.shape == (8, 2) and st[:, 0].max() == 1.0 + 0.1 * 7 and st[:, 1].sum() == 3584
+    assert (st[:, 1] == 448).all()
+    np.testing.assert_array_equal(got["c5_seeds"].ravel(), np.arange(8 * 1024, dtype=np.float64))
+    assert got["c5_stats"][:, 0].max() == 32.0
+    assert len(got["blocks"]) == 8
+    for r, blk in enumerate(got["blocks"]):
+        v = D.result_views(torch.from_numpy(blk), 4, 3, 2)
+        assert (v["x"] == r).all() and (v["evals"] == r + 1).all() and (v["y"] == 0).all()
 
 
 def test_gather_ragged_validates_shard_size():

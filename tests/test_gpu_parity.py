@@ -818,6 +818,55 @@ def test_dropin_plan_cache_reuse_is_exact():
             np.testing.assert_array_equal(gmt.v, fmt.v)
 
 
+OVERLAP_CASES = [
+    # (case, B, modes): C2's call (throughput shape, 98 MB of results); a batch in the latency
+    # shape (4, 512) with both optimisers; the streaming kernel (N = 10000)
+    ("cmap1_n2000", 1024, (True, False)),
+    ("cmap1_n2000", 128, (True, True)),
+    ("oval_n10000", 32, (True, True)),
+]
+
+
+@pytest.mark.parametrize("name,B,modes", OVERLAP_CASES)
+def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
+    """rl_optimize's overlapped download (results > 8 MiB): every instance signals its
+    completion and groups of finished instances are copied out while later ones compute.
+    The columns, counters and laps equal the plan path's (rl_plan_run + rl_plan_fetch, no
+    flags) and the stream-ordered download's (RL_OVERLAP_DOWNLOAD=0) bit for bit, and every
+    group was queued on its instances' flags (none waited for the kernel's end)."""
+    lib = _lib_or_skip()
+    case = O.load_case(name)
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    seeds = np.arange(B, dtype=np.uint64)
+    mc_on, mt_on = modes
+    mode_bits = (abi.RL_MODE_MINCURV if mc_on else 0) | (abi.RL_MODE_MINTIME if mt_on else 0)
+    pl = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=mode_bits)
+    pl.run()
+    ref = pl.fetch()
+    pl.close()
+    got = []
+    for _ in range(2):                       # a cold and a cached entry (the flags' epochs advance)
+        got.append(raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on))
+        g, s = C.c_int32(-1), C.c_int32(-1)
+        assert lib.rl_last_call_download(C.byref(g), C.byref(s)) == 0
+        assert g.value == 16 * sum(modes) and s.value == g.value, (g.value, s.value)
+    monkeypatch.setenv("RL_OVERLAP_DOWNLOAD", "0")
+    got.append(raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on))
+    g = C.c_int32(-1)
+    assert lib.rl_last_call_download(C.byref(g), None) == 0 and g.value == 0
+    lib.rl_release_plan_cache()
+    for gmc, gmt in got:
+        for r, x in zip(ref, (gmc, gmt)):
+            if r is None:
+                assert x is None
+                continue
+            for f in abi.OUT_F64 + ("evals", "accepts"):
+                np.testing.assert_array_equal(getattr(x, f), getattr(r, f), err_msg=f)
+        if mt_on:
+            for f in ("v", "ax", "lap", "vpass_sweeps"):
+                np.testing.assert_array_equal(getattr(gmt, f), getattr(ref[1], f), err_msg=f)
+
+
 def test_plan_cache_budget_and_times(monkeypatch):
     """The plan cache counts device and pinned bytes against its budget: a call whose plan
     alone exceeds RL_PLAN_CACHE_MB leaves no idle entry (and no memory) behind; within the
