@@ -196,7 +196,9 @@ __device__ __forceinline__ void ring_rays(const RingDesc& R, const double (&qx)[
             }
             if (__any(need)) visit |= 1u << q;
         }
-        if (threadIdx.x % 64 == 0) { RL_CNT(0, 4); RL_CNT(1, __popc(visit)); }
+        // (block slots per 32-entry word: 32 / RL_BLK; round 5 counted 4, the blocks-of-8
+        // figure, which halved the visited fractions reported at blocks of 16)
+        if (threadIdx.x % 64 == 0) { RL_CNT(0, 32 / RL_BLK); RL_CNT(1, __popc(visit)); }
         if (visit == 0u) { prev_ok = false; continue; }
 #pragma unroll
         for (int q = 0; q < 32 / RL_BLK; ++q) {
@@ -364,7 +366,7 @@ __device__ __forceinline__ void ring_mindist(const RingDesc& R, const double (&q
     // pass 2: candidates and the exact distances
     for (int b0 = 0; b0 < R.M; b0 += 32) {
         const uint32_t visit = visit_of(b0);
-        if (threadIdx.x % 64 == 0) { RL_CNT(4, 4); RL_CNT(5, __popc(visit)); }
+        if (threadIdx.x % 64 == 0) { RL_CNT(4, 32 / RL_BLK); RL_CNT(5, __popc(visit)); }
         if (visit == 0u) continue;
         uint32_t w = 0u;
 #pragma unroll

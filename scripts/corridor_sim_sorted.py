@@ -17,10 +17,17 @@ Groupings of the same samples into 128-sample waves:
   per_lane  lower bound of any per-sample scheme: each sample's own visited blocks (what a
             per-lane work list would test; it pays per-lane loads instead of uniform ones)
 
-Paths: C5's problem (the N = 10000 oval), seeds 1 and 7, the path P entering outer k = 1..13
-(the CPU oracle run with max_outer_iters = k: its x, y are the path after k outers; the
-corridor of outer k uses its normals).  Ground truth for `natural`: the RL_COUNT counters of
-the GPU kernel (profiles/r05/corridor_counts_c5_c2.log: 0.108 / 0.236 = 0.458 of ray blocks).
+Paths: C5's problem (the N = 10000 oval), seeds 1 and 7.  The kernel's 14 corridor passes
+(outers 0..13) see two paths: the centre line (outer 0), then the path the seeded first
+outer iteration left, which no later outer moves (its corridor collapses: every trial is
+rejected, E_k = 21) -- the CPU oracle run with max_outer_iters = 1 gives it.  Ground truth
+for `natural`: the RL_COUNT counters of the GPU kernel per pass (scripts/counts_c5_outer.py,
+profiles/r06/corridor_counts_c5_per_pass.log): first pass 0.177 and later passes 0.500 as
+logged, i.e. 0.354 and 0.999 once the counters' denominator is corrected (they counted 4
+block slots per 32-entry word, the blocks-of-8 figure, against 2 at blocks of 16; fixed in
+rl_corridor.h).  The simulation's `natural` reproduces both (0.354 / 0.998).  So the
+round-5 reading "the union scan visits 46 % of C5's ray blocks" was wrong: it visits all of
+them on the jittered path.
 
 Decision rule: build only if a grouping predicts >= 25 % fewer executed side
 tests AND fewer per-wave uniform loads than `natural` (the regrouping itself -- a sort of
@@ -80,30 +87,38 @@ def main():
     case = O.load_case("oval_n10000")
     prob, cfg = O.case_problem(case), O.case_cfg(case)
     rings = [prob.inner_seg, prob.outer_seg]
-    res = {"natural": [], "theta": [], "hough4": [], "hough9": [], "hough16": [], "per_lane": []}
+    keys = ["natural", "theta", "hough4", "hough9", "hough16", "per_lane"]
+
+    def fractions(P):
+        n = normals(P)
+        V = visits(P, n, rings)
+        th = np.mod(np.arctan2(n[:, 1], n[:, 0]), np.pi)
+        out = {"natural": union_fraction(V, np.arange(len(P))), "theta": union_fraction(V, np.argsort(th))}
+        for ct in (4, 9, 16):
+            out[f"hough{ct}"] = union_fraction(V, hough_order(P, n, ct))
+        out["per_lane"] = float(V.mean())
+        return out
+
+    centre = fractions(prob.center.copy())
+    print(json.dumps({"path": "centre (pass 0)", **{k: round(v, 4) for k, v in centre.items()}}), flush=True)
+    later = []
     for seed in (1, 7):
-        for k in range(1, 14, 3):
-            c = abi_cfg(cfg, k)
-            mc, _ = O.run_oracle(prob, c, seeds=[seed], B=1, modes=(True, False))
-            P = np.stack([mc.x[0], mc.y[0]], 1)
-            n = normals(P)
-            V = visits(P, n, rings)
-            N = len(P)
-            res["natural"].append(union_fraction(V, np.arange(N)))
-            th = np.mod(np.arctan2(n[:, 1], n[:, 0]), np.pi)
-            res["theta"].append(union_fraction(V, np.argsort(th)))
-            for ct in (4, 9, 16):
-                res[f"hough{ct}"].append(union_fraction(V, hough_order(P, n, ct)))
-            res["per_lane"].append(V.mean())
-            print(json.dumps({"seed": seed, "outer": k, **{key: round(v[-1], 4) for key, v in res.items()}}), flush=True)
-    mean = {k: float(np.mean(v)) for k, v in res.items()}
+        mc, _ = O.run_oracle(prob, abi_cfg(cfg, 1), seeds=[seed], B=1, modes=(True, False))
+        f = fractions(np.stack([mc.x[0], mc.y[0]], 1))
+        later.append(f)
+        print(json.dumps({"path": f"seed {seed} after outer 0 (passes 1-13)", **{k: round(v, 4) for k, v in f.items()}}),
+              flush=True)
+    # the kernel's 14 passes: 1 on the centre line, 13 on the jittered path
+    mean = {k: (centre[k] + 13 * float(np.mean([f[k] for f in later]))) / 14 for k in keys}
     best = min((k for k in mean if k not in ("natural", "per_lane")), key=lambda k: mean[k])
     saving = 1.0 - mean[best] / mean["natural"]
-    print(json.dumps({"mean_visited_fraction": {k: round(v, 4) for k, v in mean.items()},
-                      "counters_natural": 0.458, "best_regrouping": best,
-                      "side_test_saving_best": round(saving, 4),
+    print(json.dumps({"pass_weighted_visited_fraction": {k: round(v, 4) for k, v in mean.items()},
+                      "counters_natural_corrected": {"first_pass": 0.3544, "later_passes": 0.9992},
+                      "best_regrouping": best, "side_test_saving_best": round(saving, 4),
                       "per_lane_bound_saving": round(1.0 - mean["per_lane"] / mean["natural"], 4),
-                      "decision": "build" if saving >= 0.25 else "do not build (< 25 % fewer side tests)"}),
+                      "decision": ("build" if saving >= 0.25 else
+                                   "do not build: no wave-uniform regrouping reaches 25 % fewer side tests; the "
+                                   "per-lane bound (a work list) needs per-lane loads, built in round 5 and slower")}),
           flush=True)
 
 

@@ -9,6 +9,9 @@
 //   read8nbr   the same plus the i-1 / i+1 neighbour loads of the stencil passes
 //              (re-reads of lines the wave just loaded)             bytes = n*8 (unique)
 //   read16     one double2 per lane (the guide's calibrated width)  bytes = n*8
+//   read8buf   read8 through a buffer resource per workgroup (raw buffer loads, the
+//              streaming kernel's state path since round 5)  bytes = n*8
+//   read8nbrbuf  read8nbr through the same buffer resource              bytes = n*8 (unique)
 //   write8     one double per lane stored, same mapping              bytes = n*8
 //   write16    one double2 per lane stored                          bytes = n*8
 // Each kernel writes at most one double per workgroup besides its stores.
@@ -35,6 +38,29 @@ __global__ __launch_bounds__(TS) void read8nbr(const double* __restrict__ a, lon
     for (long i = threadIdx.x; i < chunk; i += TS) {
         const long im = i > 0 ? i - 1 : chunk - 1, ip = i + 1 < chunk ? i + 1 : 0;
         acc += s[im] * 0.25 + s[i] * 0.5 + s[ip] * 0.25;
+    }
+    if (acc == 1.2345e300) out[blockIdx.x] = acc;
+}
+
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, long i) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0));
+}
+
+__global__ __launch_bounds__(TS) void read8buf(const double* __restrict__ a, long chunk, double* out) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(a + (long)blockIdx.x * chunk), (short)0,
+                                                                       (int)(chunk * 8), 0x00020000);
+    double acc = 0.0;
+    for (long i = threadIdx.x; i < chunk; i += TS) acc += bload(r, i);
+    if (acc == 1.2345e300) out[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(TS) void read8nbrbuf(const double* __restrict__ a, long chunk, double* out) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(a + (long)blockIdx.x * chunk), (short)0,
+                                                                       (int)(chunk * 8), 0x00020000);
+    double acc = 0.0;
+    for (long i = threadIdx.x; i < chunk; i += TS) {
+        const long im = i > 0 ? i - 1 : chunk - 1, ip = i + 1 < chunk ? i + 1 : 0;
+        acc += bload(r, im) * 0.25 + bload(r, i) * 0.5 + bload(r, ip) * 0.25;
     }
     if (acc == 1.2345e300) out[blockIdx.x] = acc;
 }
@@ -89,6 +115,8 @@ int main(int argc, char** argv) {
     };
     timed("read8", [&] { hipLaunchKernelGGL(read8, dim3(blocks), dim3(TS), 0, 0, a, chunk, out); });
     timed("read8nbr", [&] { hipLaunchKernelGGL(read8nbr, dim3(blocks), dim3(TS), 0, 0, a, chunk, out); });
+    timed("read8buf", [&] { hipLaunchKernelGGL(read8buf, dim3(blocks), dim3(TS), 0, 0, a, chunk, out); });
+    timed("read8nbrbuf", [&] { hipLaunchKernelGGL(read8nbrbuf, dim3(blocks), dim3(TS), 0, 0, a, chunk, out); });
     timed("read16", [&] { hipLaunchKernelGGL(read16, dim3(blocks), dim3(TS), 0, 0, (const double2*)a, chunk / 2, out); });
     timed("write8", [&] { hipLaunchKernelGGL(write8, dim3(blocks), dim3(TS), 0, 0, a, chunk); });
     timed("write16", [&] { hipLaunchKernelGGL(write16, dim3(blocks), dim3(TS), 0, 0, (double2*)a, chunk / 2); });

@@ -867,6 +867,30 @@ def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
                 np.testing.assert_array_equal(getattr(gmt, f), getattr(ref[1], f), err_msg=f)
 
 
+def test_overlapped_download_lap_eval(monkeypatch):
+    """rl_lap_eval shares rl_optimize's cached path: 256 lap evaluations of N = 2000 paths
+    (32 MB of results) take the overlapped download, every group flag-signalled, and equal
+    the stream-ordered download bit for bit; a sample equals the CPU oracle's laps."""
+    lib = _lib_or_skip()
+    case = O.load_case("cmap1_n2000")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    rng = np.random.default_rng(5)
+    B = 256
+    P = np.repeat(prob.center[None], B, axis=0) + rng.normal(0.0, 0.05, (B, prob.N, 2))
+    got = raceline.lap_eval(P, prob.L, True, cfg)
+    g, s = C.c_int32(-1), C.c_int32(-1)
+    assert lib.rl_last_call_download(C.byref(g), C.byref(s)) == 0
+    assert g.value == 16 and s.value == 16, (g.value, s.value)
+    monkeypatch.setenv("RL_OVERLAP_DOWNLOAD", "0")
+    ref = raceline.lap_eval(P, prob.L, True, cfg)
+    for f in ("heading", "kappa", "v", "ax", "lap", "vpass_sweeps"):
+        np.testing.assert_array_equal(getattr(got, f), getattr(ref, f), err_msg=f)
+    for b in (0, B - 1):
+        orc = O.run_oracle_lap_eval(P[b], float(prob.L), True, cfg)
+        assert abs(orc.lap[0] - got.lap[b]) <= 1e-9 * orc.lap[0]
+    lib.rl_release_plan_cache()
+
+
 def test_plan_cache_budget_and_times(monkeypatch):
     """The plan cache counts device and pinned bytes against its budget: a call whose plan
     alone exceeds RL_PLAN_CACHE_MB leaves no idle entry (and no memory) behind; within the
