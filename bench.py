@@ -478,9 +478,15 @@ def run_c5(world, rank, local, dev, dist):
             "frac": round(pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pmc else None,
             "basis": "measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE x1, separate --pmc passes, "
                      "profiles/pmc_traffic.json at these kernel sources) / kernel time",
-            "counter_calibration": "x2 / x1 measured at this kernel's own 8-B/lane streaming width on a 2 GiB array "
-                                   "(scripts/fetch_calib.hip; profiles/r05/fetch_calib.json: read8 2.000, read16 "
-                                   "2.000, write8 1.000)",
+            "counter_calibration": "x2 / x1 measured at this kernel's own 8-B/lane streaming width on a 2 GiB array, "
+                                   "through plain and buffer-resource loads (scripts/fetch_calib.hip; "
+                                   "profiles/r06/fetch_calib.json: read8 2.000, read8buf 2.000, write8 1.000); the "
+                                   "stencil passes' i-1/i+1 neighbour pattern counts 1.872 (plain) / 1.886 (buffer), "
+                                   "so frac_range gives the fraction with x1.886 and x2 (ADVICE r5)",
+            "frac_range": ([round((1.886 * pmc["fetch_bytes_raw"] + pmc["write_bytes"]) / (k_ms * 1e-3) / 1e9
+                                  / HBM_PEAK_GBS, 4),
+                            round(pmc["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)]
+                           if pmc else None),
             "pmc_profile": pmc.get("profile") if pmc else None,
             "model_GBps_aside": round(model / (k_ms * 1e-3) / 1e9, 1),
             "model_note": "SURVEY §8d one-pass-per-evaluation streaming bytes; batched backtracking reads the state "

@@ -74,5 +74,5 @@ if "--commit" in sys.argv and "hbm_bytes_per_launch" in der:
               "write_bytes": der["write_bytes"], "kernel": meta.get("kernel"), "source_sha": source_sha(),
               "profile": prof, "fp64_flops_per_launch": der.get("fp64_flops_per_launch"),
               "valu_fp64_share": der.get("valu_fp64_share"),
-              "note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE x1, separate --pmc passes; both factors calibrated at this kernel family's 8-B/lane access width on a 2 GiB array (profiles/r05/fetch_calib.json: read 2.000, write 1.000)"}
+              "note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE x1, separate --pmc passes; both factors calibrated at this kernel family's 8-B/lane access width on a 2 GiB array, plain and buffer-resource loads (profiles/r06/fetch_calib.json: read 2.000, write 1.000; the neighbour-load pattern 1.886)"}
     json.dump(d, open(p, "w"), indent=1)
