@@ -581,10 +581,28 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
             g, sg = C.c_int32(), C.c_int32()
             lib.rl_last_call_download(C.byref(g), C.byref(sg))
             ks.append((run.value, kmc.value, cm.value, g.value, sg.value))
+        # the same calls into output arrays the caller keeps (pages already present)
+        keep = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
+        tr, kr = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            raceline.optimize_batch(prob, cfg, seeds, B, mintime=False, out=keep)
+            tr.append(time.perf_counter() - t0)
+            run, kmc, cm = C.c_float(), C.c_float(), C.c_float()
+            lib.rl_last_call_times(C.byref(run), C.byref(kmc), None, C.byref(cm))
+            kr.append((kmc.value, cm.value))
+        del keep
     finally:
         os.sched_setaffinity(0, prev)
     t = float(np.median(ts))
+    reused = {"call_ms_median": round(float(np.median(tr)) * 1e3, 2),
+              "outer_iters_per_s": round(B * MO / float(np.median(tr)), 1),
+              "kernel_ms_median": round(float(np.median([k for k, _ in kr])), 3),
+              "abi_call_ms_median": round(float(np.median([c for _, c in kr])), 3),
+              "note": "output arrays allocated once and passed to every call (optimize_batch(out=...)): "
+                      "no page faults in the copies, and the next kernel is not slowed (DESIGN §3g)"}
     return {"call_ms_median": round(t * 1e3, 2), "outer_iters_per_s": round(B * MO / t, 1),
+            "reused_outputs": reused,
             "call_ms_all": [round(x * 1e3, 2) for x in ts],
             "run_bracket_ms_median": round(float(np.median([k[0] for k in ks])), 3),
             "kernel_ms_median": round(float(np.median([k[1] for k in ks])), 3),
@@ -592,8 +610,9 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
             "download_groups": int(ks[-1][3]), "download_groups_signalled_min": int(min(k[4] for k in ks)),
             "host_cores": len(cores),
             "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8),
-            "note": "kernel_ms is the optimiser after the GPU's idle gap between calls (DESIGN §3e); the "
-                    "download of each group of 64 finished instances overlaps the later instances' compute"}
+            "note": "fresh numpy outputs per call (freed after it); kernel_ms is the optimiser in this call "
+                    "pattern, slower than back to back (DESIGN §3g); the download of each group of 64 finished "
+                    "instances overlaps the later instances' compute"}
 
 
 def run_step6(world, rank):

@@ -969,7 +969,7 @@ size_t cache_budget() {
     if (end == s) return kCacheBytesDefault;
     return (size_t)mb << 20;
 }
-constexpr int kJobEvents = 256;   // download events of an entry (download_staged, download_overlapped)
+constexpr int kJobEvents = 512;   // download events of an entry (download_staged, download_overlapped)
 
 struct CacheEntry {
     rl_plan* p = nullptr;
@@ -1207,9 +1207,23 @@ void populate_write(void* p, size_t n) {
 #define MADV_POPULATE_WRITE 23
 #endif
     static const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    if (!n) return;
     const uintptr_t a = (uintptr_t)p & ~(pg - 1), b = ((uintptr_t)p + n + pg - 1) & ~(pg - 1);
-    if (n) (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+    (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
 }
+
+#ifdef RL_OVL_TRACE
+// diagnostic builds: times (ms since the call's entry) of one rl_optimize call, printed to
+// stderr as one JSON line when the call returns
+struct OvlTrace {
+    std::chrono::steady_clock::time_point t0;
+    double launched = -1, kend = -1, dma = -1, copied = -1;
+    int nthr = 0;
+    std::vector<double> pub;
+};
+thread_local OvlTrace g_tr;
+double tr_ms() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_tr.t0).count(); }
+#endif
 
 // jm[m]: mode m's download jobs (out_jobs order, every array instance-major over the plan's B
 // instances).  Called after rl_plan_run queued the kernels with p->done set.
@@ -1221,10 +1235,7 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
         int s0, s1;                                    // its slices [s0, s1)
     };
     struct Slice {
-        void* pin;
-        const void* src;
-        size_t bytes;
-        int ev;                                        // event recorded after its copy
+        int ev;                                        // event recorded after its copy (-1: not queued)
     };
     struct Piece {
         unsigned char* dst;
@@ -1245,8 +1256,8 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
             job_off[m].push_back(off);
             off += (j.bytes + 255) & ~(size_t)255;
         }
-    // slices in publication order (group-major); one event per slice while they fit, else
-    // one per group (the group's last slice)
+    // slices in publication order (group-major): slice g.s0 + k is array k of group g; its
+    // event is assigned when its copy is queued
     std::vector<Slice> slices;
     std::vector<Piece> pieces;
     const size_t kPiece = (size_t)1 << 20;
@@ -1256,17 +1267,13 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
             const CopyJob& j = jm[g.m][k];
             const size_t row = j.bytes / (size_t)B;    // bytes of one instance
             const size_t o = (size_t)g.b0 * row, n = (size_t)(g.b1 - g.b0) * row;
-            if (!n) continue;
             const int si = (int)slices.size();
-            slices.push_back({e->pin + job_off[g.m][k] + o, (const unsigned char*)j.src + o, n, -1});
+            slices.push_back({-1});
             for (size_t q = 0; q < n; q += kPiece)
                 pieces.push_back({(unsigned char*)j.dst + o + q, e->pin + job_off[g.m][k] + o + q, std::min(kPiece, n - q), si});
         }
         g.s1 = (int)slices.size();
     }
-    const bool per_slice = slices.size() <= (size_t)kJobEvents;
-    for (size_t gi = 0; gi < groups.size(); ++gi)
-        for (int si = groups[gi].s0; si < groups[gi].s1; ++si) slices[si].ev = per_slice ? si : (int)gi;
     std::atomic<size_t> next{0}, next_pop{0};
     std::atomic<int> published{0};                     // slices queued (publication order)
     std::atomic<bool> bad{false};
@@ -1302,12 +1309,15 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
     bool joined[2] = {false, false};
     int signalled = 0;
 #ifdef RL_OVL_TRACE     // diagnostic builds: when each group was queued, and the kernel's end
-    const auto tr0 = std::chrono::steady_clock::now();
-    auto tr_ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(); };
-    std::vector<double> tr_pub(groups.size(), -1.0);
-    double tr_end = -1.0;
+    g_tr.pub.assign(groups.size(), -1.0);
 #endif
-    for (size_t gi = 0; gi < groups.size() && !bad.load(); ++gi) {
+    auto group_done = [&](const Group& g) {
+        for (int b = g.b0; b < g.b1; ++b)
+            if (fl[(size_t)g.m * B + b] != epoch) return false;
+        return true;
+    };
+    int next_ev = 0;
+    for (size_t gi = 0; gi < groups.size() && !bad.load();) {
         const Group& g = groups[gi];
         for (int b = g.b0;;) {
             while (b < g.b1 && fl[(size_t)g.m * B + b] == epoch) ++b;
@@ -1327,33 +1337,44 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
             std::this_thread::yield();
         }
         if (bad.load()) break;
-        for (int si = g.s0; si < g.s1 && !bad.load(); ++si) {
-            const Slice& sl = slices[si];
-            if (hipMemcpyAsync(sl.pin, sl.src, sl.bytes, hipMemcpyDeviceToHost, e->dl) != hipSuccess ||
-                (per_slice && hipEventRecord(e->ev[sl.ev], e->dl) != hipSuccess))
+        // the batch: this group and every following group of the mode that is complete too
+        // (after the kernel's end, all of them) -- one copy per array over the batch, so a
+        // burst of finishing instances moves as few large copies (1 MB copies ran at ~21 GB/s,
+        // against 56 GB/s for large ones: round-6 trace)
+        size_t ge = gi + 1;
+        while (ge < groups.size() && groups[ge].m == g.m && (joined[g.m] || group_done(groups[ge]))) ++ge;
+        const Group& gl = groups[ge - 1];
+        for (size_t k = 0; k < jm[g.m].size() && !bad.load(); ++k) {
+            const CopyJob& j = jm[g.m][k];
+            const size_t row = j.bytes / (size_t)B;
+            const size_t o = (size_t)g.b0 * row, n = (size_t)(gl.b1 - g.b0) * row;
+            const int ev = std::min(next_ev++, kJobEvents - 1);   // (a reused event only waits longer)
+            if (hipMemcpyAsync(e->pin + job_off[g.m][k] + o, (const unsigned char*)j.src + o, n, hipMemcpyDeviceToHost,
+                               e->dl) != hipSuccess ||
+                hipEventRecord(e->ev[ev], e->dl) != hipSuccess)
                 bad = true;
+            for (size_t h = gi; h < ge; ++h) slices[groups[h].s0 + k].ev = ev;
         }
-        if (!per_slice && !bad.load() && hipEventRecord(e->ev[gi], e->dl) != hipSuccess) bad = true;
         if (bad.load()) break;
-        published.store(g.s1, std::memory_order_release);
-        if (!joined[g.m]) ++signalled;
+        published.store(gl.s1, std::memory_order_release);
+        for (size_t h = gi; h < ge; ++h) {
+            if (!joined[g.m]) ++signalled;
 #ifdef RL_OVL_TRACE
-        tr_pub[gi] = tr_ms();
+            g_tr.pub[h] = tr_ms();
 #endif
+        }
+        gi = ge;
     }
 #ifdef RL_OVL_TRACE
-    if (hipEventSynchronize(p->ev_end[groups.back().m]) == hipSuccess) tr_end = tr_ms();
+    if (hipEventSynchronize(p->ev_end[groups.back().m]) == hipSuccess) g_tr.kend = tr_ms();
+    if (!slices.empty() && slices.back().ev >= 0 && hipEventSynchronize(e->ev[slices.back().ev]) == hipSuccess)
+        g_tr.dma = tr_ms();
+    g_tr.nthr = nthr;
 #endif
     work(false);
     for (auto& t : th) t.join();
 #ifdef RL_OVL_TRACE
-    {
-        const double tr_copy = tr_ms();
-        hipStreamSynchronize(e->dl);
-        std::fprintf(stderr, "{\"ovl_trace\": {\"kernel_end_seen_ms\": %.3f, \"copies_done_ms\": %.3f, \"published_ms\": [", tr_end, tr_copy);
-        for (size_t i = 0; i < tr_pub.size(); ++i) std::fprintf(stderr, "%s%.3f", i ? ", " : "", tr_pub[i]);
-        std::fprintf(stderr, "]}}\n");
-    }
+    g_tr.copied = tr_ms();
 #endif
     const bool synced = hipStreamSynchronize(e->dl) == hipSuccess;
     if (bad.load() || !synced) return fail(RL_EHIP, "download (overlapped) failed");
@@ -1367,6 +1388,10 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
 int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const uint64_t* seeds, int32_t B,
                int32_t modes, const double* centers, const double* Ls, rl_out* out_mc, rl_out* out_mt, float* kms) {
     const auto t0 = std::chrono::steady_clock::now();
+#ifdef RL_OVL_TRACE
+    g_tr = OvlTrace{};
+    g_tr.t0 = t0;
+#endif
     g_last_kernel_ms = g_last_call_ms = g_last_mode_ms[0] = g_last_mode_ms[1] = -1.0f;
     g_last_groups = g_last_groups_signalled = 0;
     if (int rc = check_inputs(prob, cfg, n_cfg, B, modes, centers)) return rc;
@@ -1462,6 +1487,9 @@ int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const u
         for (int m = 0; m < 2; ++m) p->done[m] = jm[m].empty() ? nullptr : dflags + (size_t)m * B;
     }
     rc = rl_plan_run(p, nullptr);
+#ifdef RL_OVL_TRACE
+    g_tr.launched = tr_ms();
+#endif
     p->done[0] = p->done[1] = nullptr;                 // later runs of this plan signal nothing
     if (rc) return drop(rc);
     if (overlap) rc = download_overlapped(e, p, jm, epoch);
@@ -1479,6 +1507,13 @@ int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const u
     g_last_mode_ms[0] = ms[1];
     g_last_mode_ms[1] = ms[2];
     g_last_call_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+#ifdef RL_OVL_TRACE
+    std::fprintf(stderr, "{\"ovl_trace\": {\"launched_ms\": %.3f, \"kernel_ms\": %.3f, \"kernel_end_seen_ms\": %.3f, "
+                 "\"dma_done_ms\": %.3f, \"copies_done_ms\": %.3f, \"return_ms\": %.3f, \"threads\": %d, \"published_ms\": [",
+                 g_tr.launched, ms[1] > 0 ? ms[1] : ms[2], g_tr.kend, g_tr.dma, g_tr.copied, tr_ms(), g_tr.nthr);
+    for (size_t i = 0; i < g_tr.pub.size(); ++i) std::fprintf(stderr, "%s%.3f", i ? ", " : "", g_tr.pub[i]);
+    std::fprintf(stderr, "]}}\n");
+#endif
     return RL_OK;
 }
 

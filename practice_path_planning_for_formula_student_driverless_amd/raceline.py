@@ -106,13 +106,17 @@ def _check_batch(B: int, ncfg: int, seeds) -> None:
 
 
 def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
-                   mincurv: bool = True, mintime: bool = True, devices: Optional[Sequence[int]] = None):
+                   mincurv: bool = True, mintime: bool = True, devices: Optional[Sequence[int]] = None,
+                   out=None):
     """Optimise B instances (seed b / cfg b) of one problem on the GPU.
 
     cfgs: one RlCfg (broadcast) or a list of B.  seeds: None (all zero — the
     reference exactly) or B uint64 seeds.  devices: None (the current device) or a
     list of device indices: contiguous instance blocks, one per device
-    (rl_optimize_multi).  Returns (Outputs|None, Outputs|None).
+    (rl_optimize_multi).  out: None (fresh output arrays) or the (Outputs|None,
+    Outputs|None) of an earlier call of the same shape, written in place (a caller that
+    keeps its buffers, as the C ABI's callers own theirs).  Returns (Outputs|None,
+    Outputs|None).
     """
     cfg_arr, ncfg = abi.cfg_array(cfgs)
     if B is None:
@@ -120,8 +124,17 @@ def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
     _check_batch(B, ncfg, seeds)
     mo = int(cfg_arr[0].max_outer_iters)
     seeds_a = abi.seed_array(seeds)
-    out_mc = Outputs.alloc(B, prob.N, mo, False) if mincurv else None
-    out_mt = Outputs.alloc(B, prob.N, mo, True) if mintime else None
+    if out is not None:
+        out_mc, out_mt = out
+        for o, want, mt in ((out_mc, mincurv, False), (out_mt, mintime, True)):
+            if (o is not None) != want:
+                raise ValueError("out: one Outputs per requested mode (None for the others)")
+            if o is not None and (o.x.shape != (B, prob.N) or o.evals.shape != (B, mo) or (mt and o.lap is None)
+                                  or not all(getattr(o, f).flags.c_contiguous for f in abi.OUT_F64)):
+                raise ValueError("out: Outputs of a different shape or mode")
+    else:
+        out_mc = Outputs.alloc(B, prob.N, mo, False) if mincurv else None
+        out_mt = Outputs.alloc(B, prob.N, mo, True) if mintime else None
     c_mc = out_mc.as_c() if out_mc else None
     c_mt = out_mt.as_c() if out_mt else None
     p = prob.as_c()

@@ -164,6 +164,21 @@ def test_plan_cache_queries_without_a_call():
         assert lib.rl_last_call_download(C.byref(g), None) == abi.RL_EINVAL
 
 
+def test_optimize_batch_out_is_checked():
+    """optimize_batch(out=...) takes the Outputs of an earlier call of the same shape and mode;
+    anything else is refused before any device call."""
+    case = O.load_case("track_training_map")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    N, mo = prob.N, int(cfg.max_outer_iters)
+    with pytest.raises(ValueError):          # wrong B
+        raceline.optimize_batch(prob, cfg, None, 2, mintime=False, out=(abi.Outputs.alloc(3, N, mo, False), None))
+    with pytest.raises(ValueError):          # a min-time output missing
+        raceline.optimize_batch(prob, cfg, None, 2, out=(abi.Outputs.alloc(2, N, mo, False), None))
+    with pytest.raises(ValueError):          # a min-curvature Outputs where min-time (lap, v, ax) is needed
+        raceline.optimize_batch(prob, cfg, None, 2, mincurv=False,
+                                out=(None, abi.Outputs.alloc(2, N, mo, False)))
+
+
 def test_compute_fails_loudly_without_gpu():
     lib = abi.load_library()
     if lib.rl_device_count() > 0:

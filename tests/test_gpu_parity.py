@@ -850,6 +850,14 @@ def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
         g, s = C.c_int32(-1), C.c_int32(-1)
         assert lib.rl_last_call_download(C.byref(g), C.byref(s)) == 0
         assert g.value == 16 * sum(modes) and s.value == g.value, (g.value, s.value)
+    # into the outputs of an earlier call (optimize_batch(out=...)): written in place
+    reused = raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on)
+    for o in reused:
+        if o is not None:
+            for f in abi.OUT_F64:
+                getattr(o, f).fill(np.nan)
+    got.append(raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on, out=reused))
+    assert all(a is b for a, b in zip(got[-1], reused))
     monkeypatch.setenv("RL_OVERLAP_DOWNLOAD", "0")
     got.append(raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on))
     g = C.c_int32(-1)
