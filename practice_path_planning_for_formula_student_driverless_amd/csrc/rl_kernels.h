@@ -33,14 +33,20 @@ struct KParams {
     uint32_t epoch;
 };
 
-// The instance's completion flag: every thread's result stores are written back to memory
-// (a system-scope release fence: the L2 write-back, then the wait for it), the workgroup
-// joins, then one lane stores the epoch into the host-visible flag with a vector store.
-// Called once, at the very end of the kernel, uniformly by every thread of the workgroup.
+// The instance's completion flag: every wave waits until its own result stores have reached
+// L2 (vmcnt(0): on gfx9 a store's count drops when L2 acknowledges it), the workgroup joins,
+// then one lane writes the L2 back to memory (a system-scope release fence: buffer_wbl2 and
+// its wait; all waves of a workgroup share one CU, hence one XCD's L2) and stores the epoch
+// into the host-visible flag with a vector store.  One write-back per instance instead of one
+// per wave: C2's drop-in kernel 9.08 -> 8.98 ms (profiles/r06/ab_done_one_wb.log).  Called
+// once, at the very end of the kernel, uniformly by every thread of the workgroup.
 __device__ __forceinline__ void signal_done(uint32_t* done, int b, uint32_t epoch) {
-    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(done + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(done + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Per-instance HBM state of the large-N streaming kernel (rl_stream.hip): RL_STREAM_ARRAYS
