@@ -56,6 +56,7 @@ PKG = os.path.join(REPO, "practice_path_planning_for_formula_student_driverless_
 C4_ITEMS = 7 * 512
 C3_BATCH = 4096
 C3_SAMPLE = 128            # C3 instances whose laps the CPU oracle recomputes (strided over the batch)
+C2_BATCH = 1024            # C2 instances per GPU (the default --batch); all of rank 0's are checked
 DROPIN_CASES = ["track_" + t for t in D.C4_TRACKS] + ["cmap1_n2000"]
 
 
@@ -141,6 +142,19 @@ def _lap_worker(job):
     return out
 
 
+def _c2_worker(seeds):
+    """Pool worker (CPU only): C2's min-curvature results for a list of seeds with the C
+    oracle (every column and counter; the full-size parity check of the headline batch)."""
+    import oracle_lib as O
+
+    _, prob, cfg = load_problem("cmap1_n2000")
+    if not seeds:
+        return None
+    mc, _ = O.run_oracle(prob, cfg, seeds=list(seeds), B=len(seeds), modes=(True, False))
+    return {f: getattr(mc, f) for f in C2_PARITY_COLS}
+
+
+C2_PARITY_COLS = ("x", "y", "heading", "kappa", "alpha_total", "alpha_last", "evals", "accepts")
 ALLCORE_CORES = 16      # the host CPU share of one GPU on the box (its operator's worker-pool size)
 
 
@@ -262,6 +276,17 @@ def cpu_leg(budget_s: float) -> dict:
     with mp.get_context("spawn").Pool(workers) as pool:
         r3 = pool.map(_lap_worker, chunks(jobs, workers))
         r4 = pool.map(_lap_worker, chunks(c4_jobs, workers))
+        # the whole C2 batch of rank 0 (seeds 0..B-1) through the oracle, for the bench's
+        # full-size parity check; saved for the parent (our own file, no pickle in it)
+        nb = C2_BATCH
+        parts = [p for p in pool.map(_c2_worker, [list(range(nb))[i::workers] for i in range(workers)]) if p]
+        full = {f: np.empty((nb,) + parts[0][f].shape[1:], dtype=parts[0][f].dtype) for f in C2_PARITY_COLS}
+        for i, p in enumerate(parts):
+            for f in C2_PARITY_COLS:
+                full[f][i::workers] = p[f]
+        npz_dir = tempfile.mkdtemp(prefix="rl_c2_oracle_")
+        res["c2_oracle_npz"] = os.path.join(npz_dir, "c2_oracle.npz")
+        np.savez(res["c2_oracle_npz"], **full)
     unchunk = lambda rs, n, total: [rs[i % n][i // n] for i in range(total)]   # noqa: E731
     res["c3_oracle_laps"] = {"seeds": c3_seeds, "laps": unchunk(r3, workers, len(jobs))}
     res["c4_oracle_laps"] = unchunk(r4, workers, len(c4_jobs))
@@ -347,6 +372,31 @@ def finish_cpu_leg(proc, multicore: bool):
         return {}
     lines = out.strip().splitlines()
     return json.loads(lines[-1]) if lines else {}
+
+
+def c2_full_parity(res, npz_path) -> dict:
+    """Every column and counter of rank 0's timed C2 batch against the CPU oracle on the same
+    seeds (1e-4 x column max per instance; counters exactly).  Deletes the oracle file."""
+    import shutil
+
+    try:
+        orc = np.load(npz_path)
+        out = {"instances": int(orc["x"].shape[0]), "tolerance": "1e-4 x column max (+1e-9) per instance"}
+        worst = 0.0
+        for f in ("x", "y", "heading", "kappa", "alpha_total", "alpha_last"):
+            g = res[f].cpu().numpy() if f in res else None
+            if g is None:
+                continue
+            o = orc[f]
+            rel = np.max(np.abs(g - o), axis=1) / (np.max(np.abs(o), axis=1) + 1e-300)
+            out[f + "_max_rel"] = float(rel.max())
+            worst = max(worst, float(rel.max()))
+        ev = res["evals"].cpu().numpy()
+        out["evals_equal"] = bool(np.array_equal(ev, orc["evals"]))
+        out["instances_within_tolerance"] = worst <= 1e-4
+        return out
+    finally:
+        shutil.rmtree(os.path.dirname(npz_path), ignore_errors=True)
 
 
 def lap_delta(gpu, oracle) -> dict:
@@ -1022,6 +1072,8 @@ def main():
                 "lap_max_rel": float(np.max(np.abs(np.array(open_gpu["lap"]) - np.array(oo["lap"])) / np.abs(oo["lap"]))),
                 "evals_equal": open_gpu["evals"] == oo["evals"] and open_gpu["mt_evals"] == oo["mt_evals"]}
         extras["cpu_oracle_pool"] = cpu_res.get("oracle_pool")
+        if cpu_res.get("c2_oracle_npz") and B == C2_BATCH:
+            parity["c2_all_instances_vs_oracle"] = c2_full_parity(res, cpu_res["c2_oracle_npz"])
 
     out = {
         "metric": "PGD outer-iters/sec (N=2000 samples, closed, competition_map1, 1024 alpha-seeds/GPU, min-curv)",
