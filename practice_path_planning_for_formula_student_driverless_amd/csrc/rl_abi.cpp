@@ -1484,7 +1484,11 @@ int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const u
         }
         epoch = e->epoch;
         p->epoch = epoch;
-        for (int m = 0; m < 2; ++m) p->done[m] = jm[m].empty() ? nullptr : dflags + (size_t)m * B;
+        // (test hook RL_OVERLAP_TEST_NOSIGNAL=1: the kernels do not signal, so every group takes
+        // the stream-ordered fallback after the kernel's end -- tests/test_gpu_parity.py)
+        const char* ns = std::getenv("RL_OVERLAP_TEST_NOSIGNAL");
+        const bool nosig = ns && ns[0] == '1';
+        for (int m = 0; m < 2; ++m) p->done[m] = (jm[m].empty() || nosig) ? nullptr : dflags + (size_t)m * B;
     }
     rc = rl_plan_run(p, nullptr);
 #ifdef RL_OVL_TRACE

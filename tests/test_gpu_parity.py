@@ -875,6 +875,33 @@ def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
                 np.testing.assert_array_equal(getattr(gmt, f), getattr(ref[1], f), err_msg=f)
 
 
+def test_overlapped_download_fallback_without_signals(monkeypatch):
+    """The overlapped download's fallback: when the kernels signal no instance (test hook
+    RL_OVERLAP_TEST_NOSIGNAL=1), every group waits for the kernel's end event on the copy
+    stream; the results still equal the plan path's bit for bit and no group counts as
+    signalled."""
+    lib = _lib_or_skip()
+    case = O.load_case("cmap1_n2000")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    B = 256
+    seeds = np.arange(B, dtype=np.uint64)
+    pl = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME)
+    pl.run()
+    ref = pl.fetch()
+    pl.close()
+    monkeypatch.setenv("RL_OVERLAP_TEST_NOSIGNAL", "1")
+    got = raceline.optimize_batch(prob, cfg, seeds, B)
+    g, s = C.c_int32(-1), C.c_int32(-1)
+    assert lib.rl_last_call_download(C.byref(g), C.byref(s)) == 0
+    assert g.value == 32 and s.value == 0, (g.value, s.value)
+    for r, x in zip(ref, got):
+        for f in abi.OUT_F64 + ("evals", "accepts"):
+            np.testing.assert_array_equal(getattr(x, f), getattr(r, f), err_msg=f)
+    for f in ("v", "ax", "lap", "vpass_sweeps"):
+        np.testing.assert_array_equal(getattr(got[1], f), getattr(ref[1], f), err_msg=f)
+    lib.rl_release_plan_cache()
+
+
 def test_overlapped_download_lap_eval(monkeypatch):
     """rl_lap_eval shares rl_optimize's cached path: 256 lap evaluations of N = 2000 paths
     (32 MB of results) take the overlapped download, every group flag-signalled, and equal
