@@ -225,6 +225,13 @@ struct rl_plan {
     // download; nullptr: none) and the value the kernel stores into them
     uint32_t* done[2] = {nullptr, nullptr};
     uint32_t epoch = 0;
+    // outer iteration 0's corridor, cast once per run for the whole batch (KParams::lo0/hi0):
+    // its bounds, the cfg margin all instances share (margin_uniform), and the event the
+    // concurrent min-time stream waits for
+    double *d_lo0 = nullptr, *d_hi0 = nullptr;
+    double margin0 = 0;
+    bool margin_uniform = false;
+    hipEvent_t ev_c = nullptr;
     std::vector<void*> allocs;
 
     template <class T>
@@ -374,6 +381,7 @@ int rl_plan_destroy(rl_plan* plan) {
         if (e) hipEventDestroy(e);
     for (auto& e : plan->ev_end)
         if (e) hipEventDestroy(e);
+    if (plan->ev_c) hipEventDestroy(plan->ev_c);
     if (plan->own_stream) hipStreamDestroy(plan->own_stream);
     if (plan->aux_stream) hipStreamDestroy(plan->aux_stream);
     delete plan;
@@ -391,6 +399,14 @@ int rl_plan_create(rl_plan** out, int32_t device, const rl_problem* prob, const 
 }
 
 static int alloc_mode(rl_plan* p, int m);
+
+// the cfg margin of outer iteration 0's guard, if every instance has the same one (bitwise)
+static void set_margin(rl_plan* p, const rl_cfg* cfg, int n_cfg) {
+    p->margin0 = cfg[0].safety_margin_m;
+    p->margin_uniform = true;
+    for (int c = 1; c < n_cfg; ++c)
+        if (std::memcmp(&cfg[c].safety_margin_m, &p->margin0, sizeof(double)) != 0) p->margin_uniform = false;
+}
 
 // argument checks shared by every entry point that builds or reuses a plan (no device call)
 static int check_inputs(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, int32_t B, int32_t modes,
@@ -450,6 +466,9 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
         if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
     for (auto& e : p->ev_end)
         if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
+    if (hipEventCreateWithFlags(&p->ev_c, hipEventDisableTiming) != hipSuccess)
+        return cleanup(fail(RL_EHIP, "hipEventCreate failed"));
+    set_margin(p, cfg, n_cfg);
 
     const size_t N = (size_t)std::max(p->N, 1);
     RingHost rh[2] = {make_ring(prob->inner_seg, prob->Ei), make_ring(prob->outer_seg, prob->Eo)};
@@ -459,7 +478,8 @@ static int plan_create_ex(rl_plan** out, int32_t device, const rl_problem* prob,
     if (Ls && (rc = p->alloc(&p->d_Ls, (size_t)B))) return cleanup(rc);
     if ((rc = p->alloc(&p->d_center, centers ? 2 * N * (size_t)B : 2 * N)) || (rc = p->alloc(&p->d_vtx, 2 * Mt)) ||
         (rc = p->alloc(&p->d_rec, Mt)) || (rc = p->alloc(&p->d_flag, Mt / 32)) ||
-        (rc = p->alloc(&p->d_blk, rl::ring_blk_doubles(Mt))) || (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)))
+        (rc = p->alloc(&p->d_blk, rl::ring_blk_doubles(Mt))) || (rc = p->alloc(&p->d_cfg, (size_t)n_cfg)) || (rc = p->alloc(&p->d_seeds, (size_t)B)) ||
+        (rc = p->alloc(&p->d_lo0, N)) || (rc = p->alloc(&p->d_hi0, N)))
         return cleanup(rc);
     hipStream_t st = p->own_stream;
     if (p->N > 0 && hipMemcpyAsync(p->d_center, centers ? centers : prob->center_xy,
@@ -533,7 +553,45 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
                       (int64_t)p->B * std::max(waves_per_instance(p->N, sB, false, p->stream, cus),
                                                waves_per_instance(p->N, sB, true, p->stream, cus)) <=
                           (int64_t)8 * cus;
-    if (both) HIPCHK(hipStreamWaitEvent(p->aux_stream, p->ev[0], 0));   // everything queued before the run
+    // Outer iteration 0's corridor is the same for every instance (P = the shared centre, the
+    // problem's veh_width, one cfg margin): cast it once here, rl_corridor_kernel, and let the
+    // instances load it.  Only for batches that fill the GPU in a throughput shape (or the
+    // streaming kernel): a latency-shape batch would wait for the extra launch longer than its
+    // instances save (~1/14 of their corridor time).  RL_CORRIDOR0=0 turns it off (A/B, tests).
+    const int first_m = (p->modes & RL_MODE_MINCURV) ? 0 : 1;
+    bool pre0 = p->N > 0 && p->max_outer > 0 && p->center_stride == 0 && p->margin_uniform && p->B >= 2;
+    if (pre0 && !p->stream) {
+        const rl::Shape s = rl::pick_shape(p->N, sB, first_m == 1, cus), lat = rl::lat_shape(p->N);
+        pre0 = !(s.K == lat.K && s.T == lat.T);
+    }
+    if (pre0) {
+        const char* e = std::getenv("RL_CORRIDOR0");
+        pre0 = !(e && e[0] == '0');
+    }
+    if (pre0) {
+        HIPCHK(hipEventRecord(p->ev[1 + first_m], st));        // (inside the first mode's time)
+        rl::CorrParams c{};
+        c.center = p->d_center;
+        c.N = p->N;
+        c.closed = p->closed;
+        for (int r = 0, off = 0; r < 2; off += p->ring_M[r], ++r) {
+            c.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
+            c.ring[r].rec = p->d_rec + off;
+            c.ring[r].flag = p->d_flag + off / 32;
+            c.ring[r].blk = p->d_blk + rl::ring_blk_doubles((size_t)off);
+            c.ring[r].M = p->ring_M[r];
+            c.ring[r].E = r == 0 ? p->Ei : p->Eo;
+            c.ring[r].dl0 = p->ring_dl0[r];
+            c.ring[r].dl32 = p->ring_dl32[r];
+        }
+        c.guard = p->veh_width * 0.5 + p->margin0;              // ref:706, as the kernels form it
+        c.lo = p->d_lo0;
+        c.hi = p->d_hi0;
+        const hipError_t e = rl::launch_corridor(c, st);
+        if (e != hipSuccess) return fail(RL_EHIP, std::string("corridor launch: ") + hipGetErrorString(e));
+        HIPCHK(hipEventRecord(p->ev_c, st));
+    }
+    if (both) HIPCHK(hipStreamWaitEvent(p->aux_stream, pre0 ? p->ev_c : p->ev[0], 0));   // everything queued before
     for (int m = 0; m < 2; ++m) {
         if (!(p->modes & (1 << m))) continue;
         hipStream_t st_run = st;
@@ -583,7 +641,9 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         kp.L = p->L; kp.veh_width = p->veh_width;
         kp.done = p->done[m];
         kp.epoch = p->epoch;
-        HIPCHK(hipEventRecord(p->ev[1 + m], st));
+        kp.lo0 = pre0 ? p->d_lo0 : nullptr;
+        kp.hi0 = pre0 ? p->d_hi0 : nullptr;
+        if (!(pre0 && m == first_m)) HIPCHK(hipEventRecord(p->ev[1 + m], st));
         hipError_t e = p->stream ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
         HIPCHK(hipEventRecord(p->ev_end[m], st));
@@ -1456,6 +1516,7 @@ int run_cached(const rl_problem* prob, const rl_cfg* cfg, int32_t n_cfg, const u
         if (!up(p->d_center, centers ? centers : prob->center_xy, up_ctr) || !up(p->d_Ls, Ls, up_ls) ||
             !up(p->d_cfg, cfg, up_cfg) || !up(p->d_seeds, seeds ? seeds : sd.data(), up_seed))
             return drop(fail(RL_EHIP, "upload (staged) failed"));
+        set_margin(p, cfg, n_cfg);
     }
     rl_plan* p = e->p;
     p->modes = modes;

@@ -31,6 +31,13 @@ struct KParams {
     // done[b] once every result word of b has reached memory (signal_done below)
     uint32_t* done;
     uint32_t epoch;
+    // Outer iteration 0's corridor bounds [N] (lo, hi), computed once for the whole batch by
+    // rl_corridor_kernel on the shared centre line (rl_abi.cpp rl_plan_run), or nullptr: the
+    // first corridor is the same for every instance of a batch (P = centre, guard = the
+    // problem's veh_width * 0.5 + the cfg's margin), so the instances load it instead of each
+    // casting it again
+    const double* lo0;
+    const double* hi0;
 };
 
 // The instance's completion flag: every wave waits until its own result stores have reached

@@ -621,7 +621,9 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // fills it: slot k*T+t holds (lo, hi) of sample t*K+k.
     constexpr int CKK = CK < K ? CK : K;
     // the scan (no barrier): the chunks of the work queue, bounds into the coefficient area
-    auto corridor_scan = [&](double guard) RL_AI {
+    // pre: outer iteration 0 with the batch's precomputed bounds (KParams::lo0/hi0): the same
+    // chunks, the bounds loaded instead of cast
+    auto corridor_scan = [&](double guard, bool pre) RL_AI {
         double2* bnd = &sm.u.coef[0][0][0];
         // Several waves: chunks of 64*CKK samples from a work queue in LDS, so a wave whose
         // rays are cheap takes the next chunk instead of waiting at the barrier below for
@@ -642,6 +644,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                 qx[k] = X[i]; qy[k] = Y[i]; ux[k] = NX[i]; uy[k] = NY[i];
                 act[k] = i0 + k < N;
             }
+            if (pre) {
+#pragma unroll
+                for (int k = 0; k < CKK; ++k) {
+                    const int i = min(i0 + k, N - 1);
+                    lc[k] = p.lo0[i];
+                    hc[k] = p.hi0[i];
+                }
+            } else {
 #ifdef RL_STAMPS
             RL_STAMP(7);
             corridor_bounds<CKK, RL_MD_TIGHT != 0, RL_MD_PRUNE != 0>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard,
@@ -650,6 +660,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             corridor_bounds<CKK, RL_MD_TIGHT != 0, RL_MD_PRUNE != 0>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard,
                                                                       lc, hc);
 #endif
+            }
 #pragma unroll
             for (int k = 0; k < CKK; ++k) {
                 const int i = i0 + k;
@@ -673,8 +684,8 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         }
         __syncthreads();      // the area is written again (v-pass relaxation, coefficients)
     };
-    auto corridor = [&](double guard, double (&lo)[K], double (&hi)[K]) RL_AI {
-        corridor_scan(guard);
+    auto corridor = [&](double guard, bool pre, double (&lo)[K], double (&hi)[K]) RL_AI {
+        corridor_scan(guard, pre);
         corridor_collect(lo, hi);
     };
 
@@ -1353,6 +1364,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             }
         };
         const double guard = (outer == 0 ? p.veh_width : C.veh_width_m) * 0.5 + C.safety_margin_m;
+        const bool pre = outer == 0 && p.lo0 != nullptr;        // (uniform)
         double ka[K];
         bool ka_done = false;                                    // (uniform)
         if (outer < MO) {
@@ -1368,7 +1380,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
             }
             __syncthreads();
             if constexpr (!VSPLIT) {                             // (VSPLIT: beside the v-pass below)
-                corridor(guard, lo, hi);
+                corridor(guard, pre, lo, hi);
                 seed_alpha();
             }
         }
@@ -1415,14 +1427,14 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
                     // bundled track (N = 187-261: 3-5 chunks) fall unevenly on the other waves
                     // (phase stamps: the join waited for the wave with two; two samples per lane
                     // instead, 128-sample chunks, was slower: training_map 1.49 -> 1.56 ms)
-                    if (outer < MO) corridor_scan(guard);
+                    if (outer < MO) corridor_scan(guard, pre);
                 } else if (outer < MO) {
 #if defined(RL_STAMPS) && !defined(RL_STAMPS_EVAL)
                     const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-                    corridor_scan(guard);
+                    corridor_scan(guard, pre);
                     if (wid_u < 3) st_acc[13 + wid_u] += __builtin_amdgcn_s_memtime() - ts0;   // per-wave scan time
 #else
-                    corridor_scan(guard);
+                    corridor_scan(guard, pre);
 #endif
                 }
                 if (outer < MO) {

@@ -745,6 +745,14 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
                     qx[k] = PPT(0)[i]; qy[k] = PPT(1)[i]; ux[k] = PPT(2)[i]; uy[k] = PPT(3)[i];
                     act[k] = i0 + k < N;
                 }
+                if (outer == 0 && p.lo0) {                         // the batch's precomputed first corridor
+#pragma unroll
+                    for (int k = 0; k < RL_SCK; ++k) {
+                        const int i = min(i0 + k, N - 1);
+                        lk[k] = p.lo0[i];
+                        hk[k] = p.hi0[i];
+                    }
+                } else {
 #ifdef RL_STAMPS
                 RL_SSTAMP(7);
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk,
@@ -752,6 +760,7 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
 #else
                 corridor_bounds<RL_SCK>(p.ring[0], p.ring[1], qx, qy, ux, uy, act, guard, lk, hk);
 #endif
+                }
 #pragma unroll
                 for (int k = 0; k < RL_SCK; ++k) {
                     const int i = i0 + k;

@@ -875,6 +875,64 @@ def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
                 np.testing.assert_array_equal(getattr(gmt, f), getattr(ref[1], f), err_msg=f)
 
 
+CORRIDOR0_CASES = [
+    # (case, B, modes, per-instance margins differ): throughput shapes closed and open, the
+    # streaming kernel, a per-instance cfg sweep with one margin (the batch-wide corridor
+    # applies) and with differing margins (it does not)
+    ("cmap1_n2000", 512, abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, None),
+    ("open:cmap1_n2000", 512, abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, None),
+    ("oval_n10000", 16, abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, None),
+    ("track_competition_map_testday3", 600, abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, "same"),
+    ("track_competition_map_testday3", 600, abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME, "differ"),
+]
+
+
+@pytest.mark.parametrize("name,B,modes,margins", CORRIDOR0_CASES)
+def test_batch_first_corridor_equals_per_instance(name, B, modes, margins, monkeypatch):
+    """Outer iteration 0's corridor cast once per batch (rl_corridor_kernel, KParams::lo0/hi0)
+    gives every instance exactly the bounds it would cast itself: every column and counter
+    equals the RL_CORRIDOR0=0 run bit for bit, and the seeded instances agree with the oracle."""
+    _lib_or_skip()
+    if name.startswith("open:"):                 # C2's track as an open path (bench.open_problem)
+        case = O.load_case(name[5:])
+        cprob, cfg = O.case_problem(case), O.case_cfg(case)
+        prob = abi.Problem(center=cprob.center, L=cprob.L, inner_seg=raceline.edges_for(case["inner_ring"], False),
+                           outer_seg=raceline.edges_for(case["outer_ring"], False), veh_width=cprob.veh_width,
+                           closed=False)
+    else:
+        case = O.load_case(name)
+        prob, cfg = O.case_problem(case), O.case_cfg(case)
+    cfgs = cfg
+    if margins is not None:
+        cfgs = []
+        for k in range(B):
+            c = abi.RlCfg.from_dict(cfg.to_dict())
+            abi.set_mu(c, 0.9 + 0.6 * k / B)
+            if margins == "differ":
+                c.safety_margin_m = 0.05 + 0.01 * (k % 3)
+            cfgs.append(c)
+    seeds = np.arange(B, dtype=np.uint64)
+    got = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("RL_CORRIDOR0", v)
+        pl = raceline.Plan(prob, cfgs, seeds=seeds, B=B, modes=modes)
+        pl.run()
+        got[v] = pl.fetch()
+        pl.close()
+    for a, b in zip(got["1"], got["0"]):
+        for f in abi.OUT_F64 + ("evals", "accepts"):
+            np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    for f in ("v", "ax", "lap", "vpass_sweeps"):
+        np.testing.assert_array_equal(getattr(got["1"][1], f), getattr(got["0"][1], f), err_msg=f)
+    if margins is None and not name.startswith("oval"):
+        omc, omt = O.run_oracle(prob, cfg, seeds=[0, 3], B=2)
+        for g, r, mt in ((got["1"][0], omc, False), (got["1"][1], omt, True)):
+            sub = abi.Outputs(**{f: (getattr(g, f)[[0, 3]] if getattr(g, f) is not None else None)
+                                 for f in ("x", "y", "heading", "kappa", "alpha_total", "alpha_last", "evals",
+                                           "accepts", "v", "ax", "lap", "vpass_sweeps")})
+            compare_outputs(sub, r, mt, f"{name} seeds 0,3")
+
+
 def test_overlapped_download_fallback_without_signals(monkeypatch):
     """The overlapped download's fallback: when the kernels signal no instance (test hook
     RL_OVERLAP_TEST_NOSIGNAL=1), every group waits for the kernel's end event on the copy
