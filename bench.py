@@ -590,8 +590,19 @@ def run_dropin(local):
                 run, kmc, kmt, cm = C.c_float(), C.c_float(), C.c_float(), C.c_float()
                 lib.rl_last_call_times(C.byref(run), C.byref(kmc), C.byref(kmt), C.byref(cm))
                 k[mode].append((run.value, kmc.value if mode == "mincurv" else kmt.value, cm.value))
+        # both optimisers in one call (the ABI runs them concurrently on two streams when one
+        # kernel leaves the GPU idle): what a host that needs both pays per track
+        tb, kb = [], []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            raceline.optimize_batch(prob, cfg, None, 1)
+            tb.append(1e3 * (time.perf_counter() - t0))
+            run, cm = C.c_float(), C.c_float()
+            lib.rl_last_call_times(C.byref(run), None, None, C.byref(cm))
+            kb.append(run.value)
         med = lambda v: round(float(np.median(v)), 3)   # noqa: E731
         out[name] = {"N": prob.N, "mincurv_ms": med(t["mincurv"]), "mintime_ms": med(t["mintime"]),
+                     "both_modes_one_call_ms": med(tb), "both_modes_run_bracket_ms": med(kb),
                      "shape_KxT": {m: "x".join(map(str, abi.kernel_shape(prob.N, 1, mode)))
                                    for m, mode in (("mincurv", abi.RL_MODE_MINCURV), ("mintime", abi.RL_MODE_MINTIME))}}
         for mode in ("mincurv", "mintime"):
