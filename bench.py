@@ -669,6 +669,8 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
             "run_bracket_ms_median": round(float(np.median([k[0] for k in ks])), 3),
             "kernel_ms_median": round(float(np.median([k[1] for k in ks])), 3),
             "abi_call_ms_median": round(float(np.median([k[2] for k in ks])), 3),
+            # the Python wrapper's share: fresh numpy output arrays and ctypes marshalling
+            "python_wrapper_ms_median": round(float(np.median([1e3 * w - k[2] for w, k in zip(ts, ks)])), 3),
             "download_groups": int(ks[-1][3]), "download_groups_signalled_min": int(min(k[4] for k in ks)),
             "host_cores": len(cores),
             "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8),
