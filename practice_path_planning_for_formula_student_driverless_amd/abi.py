@@ -219,16 +219,19 @@ class Outputs:
     vpass_sweeps: Optional[np.ndarray] = None
 
     @classmethod
-    def alloc(cls, B: int, N: int, max_outer: int, mintime: bool) -> "Outputs":
-        z = lambda: np.zeros((B, N), dtype=np.float64)  # noqa: E731
+    def alloc(cls, B: int, N: int, max_outer: int, mintime: bool, zero: bool = True) -> "Outputs":
+        """Result arrays of one mode; zero=False leaves them uninitialised (np.empty), for a
+        call that writes every element (rl_optimize: every column, counter and lap)."""
+        mk = np.zeros if zero else np.empty
+        z = lambda: mk((B, N), dtype=np.float64)  # noqa: E731
         o = cls(x=z(), y=z(), heading=z(), kappa=z(), alpha_total=z(), alpha_last=z(),
-                evals=np.zeros((B, max_outer), dtype=np.int32),
-                accepts=np.zeros((B, max_outer), dtype=np.int32))
+                evals=mk((B, max_outer), dtype=np.int32),
+                accepts=mk((B, max_outer), dtype=np.int32))
         if mintime:
             o.v = z()
             o.ax = z()
-            o.lap = np.zeros(B, dtype=np.float64)
-            o.vpass_sweeps = np.zeros((B, max_outer + 1), dtype=np.int32)
+            o.lap = mk(B, dtype=np.float64)
+            o.vpass_sweeps = mk((B, max_outer + 1), dtype=np.int32)
         return o
 
     def as_c(self) -> RlOut:

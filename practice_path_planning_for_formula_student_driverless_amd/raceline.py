@@ -133,8 +133,9 @@ def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
                                   or not all(getattr(o, f).flags.c_contiguous for f in abi.OUT_F64)):
                 raise ValueError("out: Outputs of a different shape or mode")
     else:
-        out_mc = Outputs.alloc(B, prob.N, mo, False) if mincurv else None
-        out_mt = Outputs.alloc(B, prob.N, mo, True) if mintime else None
+        # every element is written by the call (no zeroing of memory about to be overwritten)
+        out_mc = Outputs.alloc(B, prob.N, mo, False, zero=False) if mincurv else None
+        out_mt = Outputs.alloc(B, prob.N, mo, True, zero=False) if mintime else None
     c_mc = out_mc.as_c() if out_mc else None
     c_mt = out_mt.as_c() if out_mt else None
     p = prob.as_c()

@@ -852,10 +852,14 @@ def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
         assert g.value == 16 * sum(modes) and s.value == g.value, (g.value, s.value)
     # into the outputs of an earlier call (optimize_batch(out=...)): written in place
     reused = raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on)
-    for o in reused:
+    for o in reused:              # poison every element: the call must write all of them
         if o is not None:
-            for f in abi.OUT_F64:
-                getattr(o, f).fill(np.nan)
+            for f in abi.OUT_F64 + ("v", "ax", "lap"):
+                if getattr(o, f) is not None:
+                    getattr(o, f).fill(np.nan)
+            for f in ("evals", "accepts", "vpass_sweeps"):
+                if getattr(o, f) is not None:
+                    getattr(o, f).fill(-12345)
     got.append(raceline.optimize_batch(prob, cfg, seeds, B, mincurv=mc_on, mintime=mt_on, out=reused))
     assert all(a is b for a, b in zip(got[-1], reused))
     monkeypatch.setenv("RL_OVERLAP_DOWNLOAD", "0")
