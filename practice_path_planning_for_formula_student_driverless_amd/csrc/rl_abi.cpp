@@ -1294,9 +1294,6 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
         int m, b0, b1;
         int s0, s1;                                    // its slices [s0, s1)
     };
-    struct Slice {
-        int ev;                                        // event recorded after its copy (-1: not queued)
-    };
     struct Piece {
         unsigned char* dst;
         const unsigned char* src;
@@ -1316,23 +1313,23 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
             job_off[m].push_back(off);
             off += (j.bytes + 255) & ~(size_t)255;
         }
-    // slices in publication order (group-major): slice g.s0 + k is array k of group g; its
-    // event is assigned when its copy is queued
-    std::vector<Slice> slices;
+    // slices in publication order (group-major): slice g.s0 + k is array k of group g;
+    // slice_ev[s] is the event recorded after its copy (set when queued, before publication)
+    std::vector<int> slice_ev;
     std::vector<Piece> pieces;
     const size_t kPiece = (size_t)1 << 20;
     for (Group& g : groups) {
-        g.s0 = (int)slices.size();
+        g.s0 = (int)slice_ev.size();
         for (size_t k = 0; k < jm[g.m].size(); ++k) {
             const CopyJob& j = jm[g.m][k];
             const size_t row = j.bytes / (size_t)B;    // bytes of one instance
             const size_t o = (size_t)g.b0 * row, n = (size_t)(g.b1 - g.b0) * row;
-            const int si = (int)slices.size();
-            slices.push_back({-1});
+            const int si = (int)slice_ev.size();
+            slice_ev.push_back(-1);
             for (size_t q = 0; q < n; q += kPiece)
                 pieces.push_back({(unsigned char*)j.dst + o + q, e->pin + job_off[g.m][k] + o + q, std::min(kPiece, n - q), si});
         }
-        g.s1 = (int)slices.size();
+        g.s1 = (int)slice_ev.size();
     }
     std::atomic<size_t> next{0}, next_pop{0};
     std::atomic<int> published{0};                     // slices queued (publication order)
@@ -1349,7 +1346,7 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
                 if (bad.load()) return;
                 std::this_thread::sleep_for(std::chrono::microseconds(10));
             }
-            if (hipEventSynchronize(e->ev[slices[si].ev]) != hipSuccess) {
+            if (hipEventSynchronize(e->ev[slice_ev[si]]) != hipSuccess) {
                 bad = true;
                 return;
             }
@@ -1413,7 +1410,7 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
                                e->dl) != hipSuccess ||
                 hipEventRecord(e->ev[ev], e->dl) != hipSuccess)
                 bad = true;
-            for (size_t h = gi; h < ge; ++h) slices[groups[h].s0 + k].ev = ev;
+            for (size_t h = gi; h < ge; ++h) slice_ev[groups[h].s0 + k] = ev;
         }
         if (bad.load()) break;
         published.store(gl.s1, std::memory_order_release);
@@ -1427,7 +1424,7 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
     }
 #ifdef RL_OVL_TRACE
     if (hipEventSynchronize(p->ev_end[groups.back().m]) == hipSuccess) g_tr.kend = tr_ms();
-    if (!slices.empty() && slices.back().ev >= 0 && hipEventSynchronize(e->ev[slices.back().ev]) == hipSuccess)
+    if (!slice_ev.empty() && slice_ev.back() >= 0 && hipEventSynchronize(e->ev[slice_ev.back()]) == hipSuccess)
         g_tr.dma = tr_ms();
     g_tr.nthr = nthr;
 #endif
