@@ -937,6 +937,41 @@ def test_batch_first_corridor_equals_per_instance(name, B, modes, margins, monke
             compare_outputs(sub, r, mt, f"{name} seeds 0,3")
 
 
+@pytest.mark.parametrize("N,B,both", [(100000, 2, False), (10000, 18, True), (4096, 43, False), (2000, 88, True),
+                                      (2000, 1500, False)])
+def test_overlapped_download_group_edges(N, B, both):
+    """Overlapped downloads at group-size edges on synthetic tracks: B = 2 (two groups of one
+    instance, N = 100000), groups of 1-2 instances, ragged groups, batches just above the
+    8 MiB threshold and a large one; bit-exact against the plan path, every group
+    flag-signalled."""
+    lib = _lib_or_skip()
+    rng = np.random.default_rng(N + B)
+    prob = _synthetic(N, True, rng)
+    cfg = abi.default_cfg()
+    cfg.max_outer_iters = 3
+    cfg.max_inner_iters = 15
+    modes = abi.RL_MODE_MINCURV | (abi.RL_MODE_MINTIME if both else 0)
+    seeds = np.arange(B, dtype=np.uint64)
+    pl = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=modes)
+    pl.run()
+    ref = pl.fetch()
+    pl.close()
+    got = raceline.optimize_batch(prob, cfg, seeds, B, mintime=both)
+    g, s = C.c_int32(-1), C.c_int32(-1)
+    assert lib.rl_last_call_download(C.byref(g), C.byref(s)) == 0
+    per_mode = min(16, B)
+    assert g.value == per_mode * (2 if both else 1) and s.value == g.value, (g.value, s.value)
+    for r, x in zip(ref, got):
+        if r is None:
+            continue
+        for f in abi.OUT_F64 + ("evals", "accepts"):
+            np.testing.assert_array_equal(getattr(x, f), getattr(r, f), err_msg=f)
+    if both:
+        for f in ("v", "ax", "lap", "vpass_sweeps"):
+            np.testing.assert_array_equal(getattr(got[1], f), getattr(ref[1], f), err_msg=f)
+    lib.rl_release_plan_cache()
+
+
 def test_overlapped_download_fallback_without_signals(monkeypatch):
     """The overlapped download's fallback: when the kernels signal no instance (test hook
     RL_OVERLAP_TEST_NOSIGNAL=1), every group waits for the kernel's end event on the copy
