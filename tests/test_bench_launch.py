@@ -56,3 +56,31 @@ def test_parent_starts_ranks_and_relays_failure():
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert "2 ranks but only 0 visible GPU" in p.stderr + p.stdout
+
+
+def test_c2_full_parity_reads_and_removes_the_oracle_file(tmp_path):
+    """bench.c2_full_parity: per-instance relative errors of every column, counters exactly,
+    and the oracle file's directory removed afterwards (CPU tensors stand in for the GPU's)."""
+    import numpy as np
+    import torch
+
+    from practice_path_planning_for_formula_student_driverless_amd import distributed as D
+
+    B, N, MO = 3, 5, 2
+    rng = np.random.default_rng(1)
+    orc = {f: rng.normal(size=(B, N)) for f in D.RESULT_F64}
+    orc["evals"] = rng.integers(1, 9, size=(B, MO)).astype(np.int32)
+    orc["accepts"] = orc["evals"] - 1
+    d = tmp_path / "orc"
+    d.mkdir()
+    path = str(d / "c2_oracle.npz")
+    np.savez(path, **orc)
+    _, res = D.alloc_result_block(B, N, MO)
+    for f in D.RESULT_F64:
+        res[f].copy_(torch.from_numpy(orc[f]))
+    res["evals"].copy_(torch.from_numpy(orc["evals"]))
+    res["kappa"][1, 2] += 1e-6 * float(np.max(np.abs(orc["kappa"][1])))
+    out = bench.c2_full_parity(res, path)
+    assert out["instances"] == B and out["evals_equal"] and out["instances_within_tolerance"]
+    assert 0 < out["kappa_max_rel"] <= 1.1e-6 and out["x_max_rel"] == 0.0
+    assert not d.exists()
