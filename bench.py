@@ -618,7 +618,8 @@ def run_dropin(local):
 def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
     """C2 through the synchronous host-buffer entry point rl_optimize (the drop-in use):
     upload, kernel, download of all result columns into fresh numpy arrays (PCIe and the
-    host copies included).  The download overlaps the kernel (rl_last_call_download: groups
+    host copies included; the arrays' buffers recycled by abi.HOST_POOL once the caller
+    drops them, with a pool-off sub-leg beside it).  The download overlaps the kernel (rl_last_call_download: groups
     of finished instances copied out while later ones compute); the C side copies the
     results out with up to 8 host threads, so this leg runs after the CPU leg, with the
     process's host cores."""
@@ -630,19 +631,27 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
     cores = sorted(HOST_CORES)[:ALLCORE_CORES] if HOST_CORES else sorted(prev)
     os.sched_setaffinity(0, set(cores))
     try:
-        for _ in range(2):           # warm-up: the cached plan, pinned staging, flags, page pools
+        for _ in range(4):           # warm-up: the cached plan, pinned staging, flags, host pool, clocks
             raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
-        ts, ks = [], []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            out = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
-            ts.append(time.perf_counter() - t0)
-            del out                  # the caller keeps its results: freeing them is not part of the call
-            run, kmc, cm = C.c_float(), C.c_float(), C.c_float()
-            lib.rl_last_call_times(C.byref(run), C.byref(kmc), None, C.byref(cm))
-            g, sg = C.c_int32(), C.c_int32()
-            lib.rl_last_call_download(C.byref(g), C.byref(sg))
-            ks.append((run.value, kmc.value, cm.value, g.value, sg.value))
+        pool = abi.HOST_POOL
+        h0, m0 = pool.hits, pool.misses
+
+        def fresh_calls():
+            ts, ks = [], []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                out = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
+                ts.append(time.perf_counter() - t0)
+                del out              # the caller keeps its results: freeing them is not part of the call
+                run, kmc, cm = C.c_float(), C.c_float(), C.c_float()
+                lib.rl_last_call_times(C.byref(run), C.byref(kmc), None, C.byref(cm))
+                g, sg = C.c_int32(), C.c_int32()
+                lib.rl_last_call_download(C.byref(g), C.byref(sg))
+                ks.append((run.value, kmc.value, cm.value, g.value, sg.value))
+            return ts, ks
+
+        ts, ks = fresh_calls()
+        pool_hits, pool_misses = pool.hits - h0, pool.misses - m0
         # the same calls into output arrays the caller keeps (pages already present)
         keep = raceline.optimize_batch(prob, cfg, seeds, B, mintime=False)
         tr, kr = [], []
@@ -654,6 +663,14 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
             lib.rl_last_call_times(C.byref(run), C.byref(kmc), None, C.byref(cm))
             kr.append((kmc.value, cm.value))
         del keep
+        # last, fresh outputs with the host pool off: every call's arrays newly mapped by numpy
+        # and unmapped after it (the round-5 wrapper's behaviour)
+        cap = pool.cap
+        pool.cap = 0
+        try:
+            tn, kn = fresh_calls()
+        finally:
+            pool.cap = cap
     finally:
         os.sched_setaffinity(0, prev)
     t = float(np.median(ts))
@@ -663,8 +680,13 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
               "abi_call_ms_median": round(float(np.median([c for _, c in kr])), 3),
               "note": "output arrays allocated once and passed to every call (optimize_batch(out=...)): "
                       "no page faults in the copies, and the next kernel is not slowed (DESIGN §3g)"}
+    no_pool = {"call_ms_median": round(float(np.median(tn)) * 1e3, 2),
+               "outer_iters_per_s": round(B * MO / float(np.median(tn)), 1),
+               "kernel_ms_median": round(float(np.median([k[1] for k in kn])), 3),
+               "note": "RL_HOST_POOL_MB=0: fresh arrays mapped by numpy every call and unmapped after it"}
     return {"call_ms_median": round(t * 1e3, 2), "outer_iters_per_s": round(B * MO / t, 1),
-            "reused_outputs": reused,
+            "reused_outputs": reused, "host_pool_off": no_pool,
+            "host_pool": {"hits": int(pool_hits), "misses": int(pool_misses), "cap_mb": round(pool.cap / 2**20)},
             "call_ms_all": [round(x * 1e3, 2) for x in ts],
             "run_bracket_ms_median": round(float(np.median([k[0] for k in ks])), 3),
             "kernel_ms_median": round(float(np.median([k[1] for k in ks])), 3),
@@ -674,9 +696,9 @@ def run_c2_pcie(prob, cfg, B, MO, rank, reps: int = 5):
             "download_groups": int(ks[-1][3]), "download_groups_signalled_min": int(min(k[4] for k in ks)),
             "host_cores": len(cores),
             "bytes_down": int(B * prob.N * 6 * 8 + B * MO * 8),
-            "note": "fresh numpy outputs per call (freed after it); kernel_ms is the optimiser in this call "
-                    "pattern, slower than back to back (DESIGN §3g); the download of each group of 64 finished "
-                    "instances overlaps the later instances' compute"}
+            "note": "fresh numpy outputs per call (freed after it), their buffers recycled by the library's "
+                    "host pool (abi.HostPool); kernel_ms is the optimiser in this call pattern (DESIGN §3g); the "
+                    "download of each group of 64 finished instances overlaps the later instances' compute"}
 
 
 def run_step6(world, rank):

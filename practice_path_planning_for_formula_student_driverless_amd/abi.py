@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
+import weakref
 from dataclasses import dataclass, fields
 from typing import Optional
 
@@ -201,6 +203,72 @@ class Problem:
         return p
 
 
+class HostPool:
+    """Recycling allocator for the host result arrays of ``optimize_batch``.
+
+    A caller of the drop-in that takes fresh arrays from every call and drops them after
+    use makes the OS fault in ~100 MB of new pages per C2-sized call and unmap the old
+    ones, and the next call's kernel runs slower behind that churn.  Arrays
+    from this pool are views of a buffer the pool keeps mapped: when the last view of an
+    array dies, its buffer returns to the pool (``weakref.finalize`` on the ctypes object
+    the views are built on) and the next call of the same size gets it back, pages already
+    resident.  An array is handed out again only after every view of it is gone, so
+    results a caller keeps are never overwritten.  At most ``cap_bytes`` of free buffers
+    are kept (``RL_HOST_POOL_MB``, default 1024; 0 disables the pool); buffers beyond the
+    cap are freed normally."""
+
+    def __init__(self, cap_bytes: int):
+        self.cap = int(cap_bytes)
+        self._free: dict = {}          # nbytes -> [uint8 buffers]
+        self._free_bytes = 0
+        self._lock = threading.Lock()
+        self.hits = 0
+        self.misses = 0
+
+    def _release(self, buf: np.ndarray) -> None:
+        # (a finalizer can run inside alloc's locked region on this thread: never block)
+        if not self._lock.acquire(blocking=False):
+            return
+        try:
+            if self._free_bytes + buf.nbytes <= self.cap:
+                self._free.setdefault(buf.nbytes, []).append(buf)
+                self._free_bytes += buf.nbytes
+        finally:
+            self._lock.release()
+
+    def empty(self, shape, dtype) -> np.ndarray:
+        """An uninitialised C-contiguous array, from a recycled buffer when one fits."""
+        dt = np.dtype(dtype)
+        nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+        if nbytes == 0 or self.cap <= 0:
+            return np.empty(shape, dtype=dt)
+        buf = None
+        with self._lock:
+            lst = self._free.get(nbytes)
+            if lst:
+                buf = lst.pop()
+                self._free_bytes -= nbytes
+        if buf is None:
+            self.misses += 1
+            buf = np.empty(nbytes, dtype=np.uint8)
+        else:
+            self.hits += 1
+        owner = (C.c_char * nbytes).from_buffer(buf)
+        weakref.finalize(owner, self._release, buf).atexit = False
+        return np.frombuffer(owner, dtype=dt).reshape(shape)
+
+    def free_bytes(self) -> int:
+        return self._free_bytes
+
+    def clear(self) -> None:
+        with self._lock:
+            self._free.clear()
+            self._free_bytes = 0
+
+
+HOST_POOL = HostPool(int(float(os.environ.get("RL_HOST_POOL_MB", "1024")) * (1 << 20)))
+
+
 @dataclass
 class Outputs:
     """Host-side SoA result buffers [B][N] for one mode."""
@@ -219,10 +287,17 @@ class Outputs:
     vpass_sweeps: Optional[np.ndarray] = None
 
     @classmethod
-    def alloc(cls, B: int, N: int, max_outer: int, mintime: bool, zero: bool = True) -> "Outputs":
-        """Result arrays of one mode; zero=False leaves them uninitialised (np.empty), for a
-        call that writes every element (rl_optimize: every column, counter and lap)."""
-        mk = np.zeros if zero else np.empty
+    def alloc(cls, B: int, N: int, max_outer: int, mintime: bool, zero: bool = True,
+              pool: Optional[HostPool] = None) -> "Outputs":
+        """Result arrays of one mode; zero=False leaves them uninitialised (np.empty, or
+        recycled buffers of ``pool``), for a call that writes every element (rl_optimize:
+        every column, counter and lap)."""
+        if zero:
+            mk = np.zeros
+        elif pool is not None:
+            mk = pool.empty
+        else:
+            mk = np.empty
         z = lambda: mk((B, N), dtype=np.float64)  # noqa: E731
         o = cls(x=z(), y=z(), heading=z(), kappa=z(), alpha_total=z(), alpha_last=z(),
                 evals=mk((B, max_outer), dtype=np.int32),

@@ -113,10 +113,11 @@ def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
     cfgs: one RlCfg (broadcast) or a list of B.  seeds: None (all zero — the
     reference exactly) or B uint64 seeds.  devices: None (the current device) or a
     list of device indices: contiguous instance blocks, one per device
-    (rl_optimize_multi).  out: None (fresh output arrays) or the (Outputs|None,
-    Outputs|None) of an earlier call of the same shape, written in place (a caller that
-    keeps its buffers, as the C ABI's callers own theirs).  Returns (Outputs|None,
-    Outputs|None).
+    (rl_optimize_multi).  out: None (fresh output arrays from abi.HOST_POOL, which
+    recycles the buffers of earlier results the caller has dropped) or the
+    (Outputs|None, Outputs|None) of an earlier call of the same shape, written in place
+    (a caller that keeps its buffers, as the C ABI's callers own theirs).  Returns
+    (Outputs|None, Outputs|None).
     """
     cfg_arr, ncfg = abi.cfg_array(cfgs)
     if B is None:
@@ -133,9 +134,10 @@ def optimize_batch(prob: Problem, cfgs, seeds=None, B: Optional[int] = None,
                                   or not all(getattr(o, f).flags.c_contiguous for f in abi.OUT_F64)):
                 raise ValueError("out: Outputs of a different shape or mode")
     else:
-        # every element is written by the call (no zeroing of memory about to be overwritten)
-        out_mc = Outputs.alloc(B, prob.N, mo, False, zero=False) if mincurv else None
-        out_mt = Outputs.alloc(B, prob.N, mo, True, zero=False) if mintime else None
+        # every element is written by the call (no zeroing of memory about to be overwritten);
+        # buffers recycled from arrays of earlier calls that the caller has dropped
+        out_mc = Outputs.alloc(B, prob.N, mo, False, zero=False, pool=abi.HOST_POOL) if mincurv else None
+        out_mt = Outputs.alloc(B, prob.N, mo, True, zero=False, pool=abi.HOST_POOL) if mintime else None
     c_mc = out_mc.as_c() if out_mc else None
     c_mt = out_mt.as_c() if out_mt else None
     p = prob.as_c()

@@ -179,6 +179,54 @@ def test_optimize_batch_out_is_checked():
                                 out=(None, abi.Outputs.alloc(2, N, mo, False)))
 
 
+def test_host_pool_recycles_only_dropped_arrays():
+    """abi.HostPool: an array's buffer returns to the pool when its last view dies, is handed
+    out again for the same size, never while any view of it lives, and the cap bounds what
+    the pool keeps (0: plain numpy arrays)."""
+    import gc
+    pool = abi.HostPool(1 << 20)
+    a = pool.empty((16, 32), np.float64)
+    assert a.shape == (16, 32) and a.dtype == np.float64 and a.flags.c_contiguous and a.flags.writeable
+    assert (pool.hits, pool.misses, pool.free_bytes()) == (0, 1, 0)
+    addr = a.ctypes.data
+    view = a[3:5, ::2]
+    del a
+    gc.collect()
+    assert pool.free_bytes() == 0                  # a view still holds the buffer
+    b = pool.empty((16, 32), np.float64)
+    assert b.ctypes.data != addr and pool.misses == 2
+    del view
+    assert pool.free_bytes() == 16 * 32 * 8
+    c = pool.empty((512,), np.int64)               # same byte size, another dtype and shape
+    assert c.ctypes.data == addr and pool.hits == 1 and pool.free_bytes() == 0
+    c[:] = 7
+    assert b.ctypes.data != c.ctypes.data
+    del b, c
+    assert pool.free_bytes() == 2 * 16 * 32 * 8
+    big = pool.empty((1 << 18,), np.float64)       # 2 MiB: beyond the 1 MiB cap when dropped
+    del big
+    assert pool.free_bytes() == 2 * 16 * 32 * 8
+    pool.clear()
+    assert pool.free_bytes() == 0
+    off = abi.HostPool(0)
+    d = off.empty((4, 4), np.float64)
+    assert d.base is None and (off.hits, off.misses) == (0, 0)
+    assert pool.empty((0, 5), np.float64).shape == (0, 5)
+
+
+def test_outputs_from_pool():
+    """Outputs.alloc(zero=False, pool=...) builds every array of a mode from the pool."""
+    pool = abi.HostPool(1 << 26)
+    o = abi.Outputs.alloc(3, 50, 14, True, zero=False, pool=pool)
+    assert o.x.shape == (3, 50) and o.evals.shape == (3, 14) and o.evals.dtype == np.int32
+    assert o.lap.shape == (3,) and o.vpass_sweeps.shape == (3, 15)
+    assert pool.misses == 12
+    del o
+    o2 = abi.Outputs.alloc(3, 50, 14, True, zero=False, pool=pool)
+    assert pool.hits == 12 and pool.free_bytes() == 0
+    assert o2.as_c().x                               # plain C pointers for the ABI
+
+
 def test_compute_fails_loudly_without_gpu():
     lib = abi.load_library()
     if lib.rl_device_count() > 0:

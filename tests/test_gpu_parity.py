@@ -827,6 +827,45 @@ OVERLAP_CASES = [
 ]
 
 
+def test_host_pool_outputs_are_exact():
+    """optimize_batch's fresh outputs come from abi.HOST_POOL: after a call's results are
+    poisoned and dropped, the next call gets the same buffers back and writes every element;
+    results a caller still holds are never handed out again.  Both optimisers, C2's problem
+    at B = 64, against the plan path bit for bit."""
+    _lib_or_skip()
+    case = O.load_case("cmap1_n2000")
+    prob, cfg = O.case_problem(case), O.case_cfg(case)
+    B = 64
+    seeds = np.arange(B, dtype=np.uint64)
+    pl = raceline.Plan(prob, cfg, seeds=seeds, B=B, modes=abi.RL_MODE_MINCURV | abi.RL_MODE_MINTIME)
+    pl.run()
+    ref = pl.fetch()
+    pl.close()
+    pool = abi.HOST_POOL
+    fields_f = abi.OUT_F64 + ("v", "ax", "lap")
+    fields_i = ("evals", "accepts", "vpass_sweeps")
+
+    def arrays(res):
+        return [getattr(o, f) for o in res for f in fields_f + fields_i if getattr(o, f) is not None]
+
+    first = raceline.optimize_batch(prob, cfg, seeds, B)
+    addrs = {a.ctypes.data for a in arrays(first)}
+    for a in arrays(first):                  # poison: the next call must overwrite all of it
+        a.fill(np.nan if a.dtype == np.float64 else -12345)
+    h0 = pool.hits
+    del first, a
+    second = raceline.optimize_batch(prob, cfg, seeds, B)
+    assert pool.hits - h0 == len(addrs)
+    assert {a.ctypes.data for a in arrays(second)} == addrs
+    third = raceline.optimize_batch(prob, cfg, seeds, B)      # second is still held
+    assert not ({a.ctypes.data for a in arrays(third)} & addrs)
+    for got in (second, third):
+        for r, x in zip(ref, got):
+            for f in fields_f + fields_i:
+                if getattr(r, f) is not None:
+                    np.testing.assert_array_equal(getattr(x, f), getattr(r, f), err_msg=f)
+
+
 @pytest.mark.parametrize("name,B,modes", OVERLAP_CASES)
 def test_overlapped_download_equals_plan(name, B, modes, monkeypatch):
     """rl_optimize's overlapped download (results > 8 MiB): every instance signals its
