@@ -1707,6 +1707,7 @@ int rl_debug_stamps_mid(unsigned long long* host, int nblocks) { return rl::debu
 // diagnostic builds only: corridor work counters of the stream kernel's translation unit
 int rl_debug_counts(unsigned long long* host, int reset) { return rl::debug_counts(host, reset); }
 int rl_debug_counts_geom(unsigned long long* host, int reset) { return rl::debug_counts_geom(host, reset); }
+int rl_debug_counts_reg(unsigned long long* host, int reset) { return rl::debug_counts_reg(host, reset); }
 #endif
 
 }  // extern "C"

@@ -151,6 +151,7 @@ int debug_stamps_mid(unsigned long long* host, int nblocks);
 #ifdef RL_COUNT
 int debug_counts(unsigned long long* host, int reset);
 int debug_counts_geom(unsigned long long* host, int reset);
+int debug_counts_reg(unsigned long long* host, int reset);
 #endif
 
 }  // namespace rl

@@ -102,6 +102,17 @@ Shape pick_shape(int N, int B, bool mintime, int cus) {
     return {8, 512};
 }
 
+#ifdef RL_COUNT
+// diagnostic builds: this translation unit's corridor counters (the throughput shapes)
+int debug_counts_reg(unsigned long long* host, int reset) {
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(rl_dbg_count), z, sizeof(z)) == hipSuccess ? 0 : -3;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rl_dbg_count), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -3;
+}
+#endif
+
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st) {
     if (p.N <= 0 || pick_k(p.N) < 0) return hipErrorInvalidValue;
 #ifdef RL_ANALYZE_ONE   // static analysis builds (scripts/regs_one.sh): the C2/C3 shape only (2: open)
