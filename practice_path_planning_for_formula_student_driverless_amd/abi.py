@@ -211,28 +211,31 @@ class HostPool:
     ones, and the next call's kernel runs slower behind that churn.  Arrays
     from this pool are views of a buffer the pool keeps mapped: when the last view of an
     array dies, its buffer returns to the pool (``weakref.finalize`` on the ctypes object
-    the views are built on) and the next call of the same size gets it back, pages already
-    resident.  An array is handed out again only after every view of it is gone, so
+    the views are built on) and the next request of the same byte size gets it back, pages
+    already resident.  An array is handed out again only after every view of it is gone, so
     results a caller keeps are never overwritten.  At most ``cap_bytes`` of free buffers
-    are kept (``RL_HOST_POOL_MB``, default 1024; 0 disables the pool); buffers beyond the
-    cap are freed normally."""
+    are kept (``RL_HOST_POOL_MB``, default 1024; 0 disables the pool): a returned buffer
+    that does not fit evicts the oldest free ones.  Arrays under ``min_bytes`` (256 KiB:
+    malloc serves them from its heap, without mapping) are plain numpy arrays."""
 
-    def __init__(self, cap_bytes: int):
+    def __init__(self, cap_bytes: int, min_bytes: int = 1 << 18):
         self.cap = int(cap_bytes)
-        self._free: dict = {}          # nbytes -> [uint8 buffers]
+        self.min_bytes = int(min_bytes)
+        self._free: list = []          # free uint8 buffers, oldest first
         self._free_bytes = 0
         self._lock = threading.Lock()
         self.hits = 0
         self.misses = 0
 
     def _release(self, buf: np.ndarray) -> None:
-        # (a finalizer can run inside alloc's locked region on this thread: never block)
-        if not self._lock.acquire(blocking=False):
+        # (a finalizer can run inside empty()'s locked region on this thread: never block)
+        if buf.nbytes > self.cap or not self._lock.acquire(blocking=False):
             return
         try:
-            if self._free_bytes + buf.nbytes <= self.cap:
-                self._free.setdefault(buf.nbytes, []).append(buf)
-                self._free_bytes += buf.nbytes
+            while self._free and self._free_bytes + buf.nbytes > self.cap:
+                self._free_bytes -= self._free.pop(0).nbytes
+            self._free.append(buf)
+            self._free_bytes += buf.nbytes
         finally:
             self._lock.release()
 
@@ -240,14 +243,15 @@ class HostPool:
         """An uninitialised C-contiguous array, from a recycled buffer when one fits."""
         dt = np.dtype(dtype)
         nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
-        if nbytes == 0 or self.cap <= 0:
+        if nbytes < self.min_bytes or nbytes > self.cap:
             return np.empty(shape, dtype=dt)
         buf = None
         with self._lock:
-            lst = self._free.get(nbytes)
-            if lst:
-                buf = lst.pop()
-                self._free_bytes -= nbytes
+            for i in range(len(self._free) - 1, -1, -1):     # the most recently returned first
+                if self._free[i].nbytes == nbytes:
+                    buf = self._free.pop(i)
+                    self._free_bytes -= nbytes
+                    break
         if buf is None:
             self.misses += 1
             buf = np.empty(nbytes, dtype=np.uint8)

@@ -184,7 +184,7 @@ def test_host_pool_recycles_only_dropped_arrays():
     out again for the same size, never while any view of it lives, and the cap bounds what
     the pool keeps (0: plain numpy arrays)."""
     import gc
-    pool = abi.HostPool(1 << 20)
+    pool = abi.HostPool(1 << 20, min_bytes=0)
     a = pool.empty((16, 32), np.float64)
     assert a.shape == (16, 32) and a.dtype == np.float64 and a.flags.c_contiguous and a.flags.writeable
     assert (pool.hits, pool.misses, pool.free_bytes()) == (0, 1, 0)
@@ -203,7 +203,8 @@ def test_host_pool_recycles_only_dropped_arrays():
     assert b.ctypes.data != c.ctypes.data
     del b, c
     assert pool.free_bytes() == 2 * 16 * 32 * 8
-    big = pool.empty((1 << 18,), np.float64)       # 2 MiB: beyond the 1 MiB cap when dropped
+    big = pool.empty((1 << 18,), np.float64)       # 2 MiB: beyond the 1 MiB cap, never pooled
+    assert big.base is None
     del big
     assert pool.free_bytes() == 2 * 16 * 32 * 8
     pool.clear()
@@ -212,11 +213,29 @@ def test_host_pool_recycles_only_dropped_arrays():
     d = off.empty((4, 4), np.float64)
     assert d.base is None and (off.hits, off.misses) == (0, 0)
     assert pool.empty((0, 5), np.float64).shape == (0, 5)
+    small = abi.HostPool(1 << 20).empty((16, 32), np.float64)   # under the default 256 KiB floor
+    assert small.base is None
+
+
+def test_host_pool_evicts_oldest_beyond_cap():
+    """A returned buffer that does not fit under the cap evicts the oldest free buffers, so
+    buffers of sizes no longer asked for do not block the ones in use."""
+    pool = abi.HostPool(3 << 16, min_bytes=0)      # room for three 64 KiB buffers
+    olds = [pool.empty((1 << 13,), np.float64) for _ in range(3)]
+    del olds
+    assert pool.free_bytes() == 3 << 16
+    news = [pool.empty((1 << 12,), np.float64) for _ in range(2)]     # 32 KiB: other size
+    assert pool.misses == 5
+    del news                                        # the first evicts the oldest 64 KiB buffer
+    assert pool.free_bytes() == 3 << 16 and len(pool._free) == 4
+    assert pool.empty((1 << 12,), np.float64).nbytes == 1 << 15 and pool.hits == 1
+    keep = [pool.empty((1 << 13,), np.float64) for _ in range(3)]   # two 64 KiB buffers left
+    assert (pool.hits, pool.misses) == (3, 6)       # the oldest was evicted: the third is new
 
 
 def test_outputs_from_pool():
     """Outputs.alloc(zero=False, pool=...) builds every array of a mode from the pool."""
-    pool = abi.HostPool(1 << 26)
+    pool = abi.HostPool(1 << 26, min_bytes=0)
     o = abi.Outputs.alloc(3, 50, 14, True, zero=False, pool=pool)
     assert o.x.shape == (3, 50) and o.evals.shape == (3, 14) and o.evals.dtype == np.int32
     assert o.lap.shape == (3,) and o.vpass_sweeps.shape == (3, 15)

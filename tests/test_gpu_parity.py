@@ -845,11 +845,14 @@ def test_host_pool_outputs_are_exact():
     fields_f = abi.OUT_F64 + ("v", "ax", "lap")
     fields_i = ("evals", "accepts", "vpass_sweeps")
 
-    def arrays(res):
-        return [getattr(o, f) for o in res for f in fields_f + fields_i if getattr(o, f) is not None]
+    def arrays(res):                          # the pooled ones (>= min_bytes: the [B][N] columns)
+        return [getattr(o, f) for o in res for f in fields_f + fields_i
+                if getattr(o, f) is not None and getattr(o, f).nbytes >= pool.min_bytes]
 
+    pool.clear()
     first = raceline.optimize_batch(prob, cfg, seeds, B)
     addrs = {a.ctypes.data for a in arrays(first)}
+    assert len(addrs) == 14                  # 6 min-curvature and 8 min-time columns
     for a in arrays(first):                  # poison: the next call must overwrite all of it
         a.fill(np.nan if a.dtype == np.float64 else -12345)
     h0 = pool.hits
