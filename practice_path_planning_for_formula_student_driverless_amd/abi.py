@@ -431,6 +431,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.rl_plan_create.restype = C.c_int
     lib.rl_plan_run.argtypes = [C.c_void_p, C.c_void_p]
     lib.rl_plan_run.restype = C.c_int
+    if path == LIB_PATH or hasattr(lib, "rl_plan_run_group"):   # (A/B builds of older sources lack it)
+        lib.rl_plan_run_group.argtypes = [C.POINTER(C.c_void_p), C.c_int32, C.c_void_p]
+        lib.rl_plan_run_group.restype = C.c_int
     lib.rl_plan_fetch.argtypes = [C.c_void_p, C.POINTER(RlOut), C.POINTER(RlOut)]
     lib.rl_plan_fetch.restype = C.c_int
     lib.rl_plan_device_outputs.argtypes = [C.c_void_p, C.c_int32, C.POINTER(RlOut)]

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <limits>
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <mutex>
@@ -536,6 +537,38 @@ static int alloc_mode(rl_plan* p, int m) {
     return RL_OK;
 }
 
+// the launch parameters of mode m (0: min-curv, 1: min-time) of plan p
+static void fill_kparams(const rl_plan* p, int m, int sB, bool pre0, rl::KParams& kp) {
+    const ModeBufs& mb = p->mb[m];
+    kp = rl::KParams{};
+    kp.center = p->d_center;
+    kp.center_stride = p->center_stride;
+    kp.Ls = p->d_Ls;
+    for (int r = 0, off = 0; r < 2; off += p->ring_M[r], ++r) {
+        kp.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
+        kp.ring[r].rec = p->d_rec + off;
+        kp.ring[r].flag = p->d_flag + off / 32;
+        kp.ring[r].blk = p->d_blk + rl::ring_blk_doubles((size_t)off);
+        kp.ring[r].M = p->ring_M[r];
+        kp.ring[r].E = r == 0 ? p->Ei : p->Eo;
+        kp.ring[r].dl0 = p->ring_dl0[r];
+        kp.ring[r].dl32 = p->ring_dl32[r];
+    }
+    kp.cfg = p->d_cfg;
+    kp.seeds = p->d_seeds;
+    kp.x = mb.x; kp.y = mb.y; kp.heading = mb.heading; kp.kappa = mb.kappa;
+    kp.alpha_total = mb.alpha_total; kp.alpha_last = mb.alpha_last;
+    kp.v = mb.v; kp.ax = mb.ax; kp.lap = mb.lap; kp.nx = mb.nx; kp.ny = mb.ny;
+    kp.evals = mb.evals; kp.accepts = mb.accepts; kp.sweeps = mb.sweeps;
+    kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
+    kp.shape_B = sB;
+    kp.L = p->L; kp.veh_width = p->veh_width;
+    kp.done = p->done[m];
+    kp.epoch = p->epoch;
+    kp.lo0 = pre0 ? p->d_lo0 : nullptr;
+    kp.hi0 = pre0 ? p->d_hi0 : nullptr;
+}
+
 int rl_plan_run(rl_plan* p, void* hip_stream) {
     if (!p) return fail(RL_EINVAL, "plan is NULL");
     HIPCHK(hipSetDevice(p->device));
@@ -617,32 +650,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
         }
         (void)BN;
         rl::KParams kp;
-        kp.center = p->d_center;
-        kp.center_stride = p->center_stride;
-        kp.Ls = p->d_Ls;
-        for (int r = 0, off = 0; r < 2; off += p->ring_M[r], ++r) {
-            kp.ring[r].vtx = (const double2*)(p->d_vtx + 2 * (size_t)off);
-            kp.ring[r].rec = p->d_rec + off;
-            kp.ring[r].flag = p->d_flag + off / 32;
-            kp.ring[r].blk = p->d_blk + rl::ring_blk_doubles((size_t)off);
-            kp.ring[r].M = p->ring_M[r];
-            kp.ring[r].E = r == 0 ? p->Ei : p->Eo;
-            kp.ring[r].dl0 = p->ring_dl0[r];
-            kp.ring[r].dl32 = p->ring_dl32[r];
-        }
-        kp.cfg = p->d_cfg;
-        kp.seeds = p->d_seeds;
-        kp.x = mb.x; kp.y = mb.y; kp.heading = mb.heading; kp.kappa = mb.kappa;
-        kp.alpha_total = mb.alpha_total; kp.alpha_last = mb.alpha_last;
-        kp.v = mb.v; kp.ax = mb.ax; kp.lap = mb.lap; kp.nx = mb.nx; kp.ny = mb.ny;
-        kp.evals = mb.evals; kp.accepts = mb.accepts; kp.sweeps = mb.sweeps;
-        kp.N = p->N; kp.Ei = p->Ei; kp.Eo = p->Eo; kp.ncfg = p->ncfg; kp.B = p->B; kp.closed = p->closed;
-        kp.shape_B = sB;
-        kp.L = p->L; kp.veh_width = p->veh_width;
-        kp.done = p->done[m];
-        kp.epoch = p->epoch;
-        kp.lo0 = pre0 ? p->d_lo0 : nullptr;
-        kp.hi0 = pre0 ? p->d_hi0 : nullptr;
+        fill_kparams(p, m, sB, pre0, kp);
         if (!(pre0 && m == first_m)) HIPCHK(hipEventRecord(p->ev[1 + m], st));
         hipError_t e = p->stream ? rl::launch_stream(kp, mb.sb, m == 1, st) : rl::launch_optimize(kp, m == 1, st);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
@@ -652,6 +660,119 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
     if (both) HIPCHK(hipStreamWaitEvent(st, p->ev_end[1], 0));
     HIPCHK(hipEventRecord(p->ev[3], st));
     p->ran = true;
+    return RL_OK;
+}
+
+// rl_plan_run of n plans (one device) as few launches as their shapes allow: every (plan,
+// mode) whose kernel shape is a one-wave throughput shape (rl::group_shape) joins the group
+// launch of its (mode, K, closed, ragged) class, up to RL_GROUP_MAX plans per launch; the
+// other plans run as rl_plan_run on their own streams.  The launches run concurrently, each
+// on a plan-owned stream after everything queued on `hip_stream`, which waits for all of
+// them.  Results equal each plan's own rl_plan_run bit for bit (the same instance code, the
+// plan's own shape); the batch-wide first corridor is left to the instances.  Every plan's
+// rl_plan_kernel_ms(.., 0) is the whole group's run, its mode times its launch's.
+int rl_plan_run_group(rl_plan* const* plans, int32_t n, void* hip_stream) {
+    if (!plans || n < 1) return fail(RL_EINVAL, "rl_plan_run_group: no plans");
+    for (int i = 0; i < n; ++i) {
+        if (!plans[i]) return fail(RL_EINVAL, "rl_plan_run_group: a plan is NULL");
+        if (plans[i]->device != plans[0]->device) return fail(RL_EINVAL, "rl_plan_run_group: plans on different devices");
+        for (int j = 0; j < i; ++j)
+            if (plans[j] == plans[i]) return fail(RL_EINVAL, "rl_plan_run_group: a plan is listed twice");
+    }
+    HIPCHK(hipSetDevice(plans[0]->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : plans[0]->own_stream;
+    const int cus = device_cus(plans[0]->device);
+    struct Item {
+        rl_plan* p;
+        int m;
+    };
+    // class key: mode, K, closed, ragged
+    std::vector<std::pair<std::array<int, 4>, std::vector<Item>>> classes;
+    std::vector<rl_plan*> solo;
+    for (int i = 0; i < n; ++i) {
+        rl_plan* p = plans[i];
+        const int sB = p->shape_B > 0 ? p->shape_B : p->B;
+        bool ok = !p->stream && p->N > 0 && p->max_outer > 0 && (p->modes & 3);
+        std::array<int, 4> key[2];
+        for (int m = 0; m < 2 && ok; ++m) {
+            if (!(p->modes & (1 << m))) continue;
+            const rl::Shape s = rl::pick_shape(p->N, sB, m == 1, cus);
+            ok = rl::group_shape(s);
+            key[m] = {m, s.K, p->closed ? 1 : 0, p->N % s.K ? 1 : 0};
+        }
+        if (!ok) {
+            solo.push_back(p);
+            continue;
+        }
+        for (int m = 0; m < 2; ++m) {
+            if (!(p->modes & (1 << m))) continue;
+            auto it = std::find_if(classes.begin(), classes.end(), [&](const auto& c) { return c.first == key[m]; });
+            if (it == classes.end()) {
+                classes.push_back({key[m], {}});
+                it = classes.end() - 1;
+            }
+            it->second.push_back({p, m});
+        }
+    }
+    // the launches: class chunks of up to RL_GROUP_MAX plans, then the solo plans
+    struct Launch {
+        int cls;
+        size_t i0;
+        int cnt;
+        hipStream_t ls;
+    };
+    std::vector<Launch> launches;
+    std::vector<hipStream_t> pool;                   // grouped plans' own and aux streams
+    for (auto& c : classes)
+        for (const Item& it : c.second)
+            for (hipStream_t x : {it.p->own_stream, it.p->aux_stream})
+                if (std::find(pool.begin(), pool.end(), x) == pool.end()) pool.push_back(x);
+    for (size_t ci = 0; ci < classes.size(); ++ci)
+        for (size_t i0 = 0; i0 < classes[ci].second.size(); i0 += rl::RL_GROUP_MAX)
+            launches.push_back({(int)ci, i0, (int)std::min<size_t>(rl::RL_GROUP_MAX, classes[ci].second.size() - i0),
+                                pool[launches.size() % pool.size()]});
+    // fork: every launch stream waits for what `hip_stream` has queued, before any launch
+    // (a solo plan's rl_plan_run re-records its own events)
+    hipEvent_t start = plans[0]->ev_c;               // (a disable-timing event of the group)
+    HIPCHK(hipEventRecord(start, st));
+    for (const Launch& L : launches) HIPCHK(hipStreamWaitEvent(L.ls, start, 0));
+    for (rl_plan* p : solo) HIPCHK(hipStreamWaitEvent(p->own_stream, start, 0));
+    for (int i = 0; i < n; ++i) {
+        HIPCHK(hipEventRecord(plans[i]->ev[0], st));
+        plans[i]->last_stream = st;
+    }
+    std::vector<hipEvent_t> ends;
+    for (const Launch& L : launches) {
+        const int m = classes[L.cls].first[0];
+        const rl::Shape s{classes[L.cls].first[1], 64};
+        const std::vector<Item>& items = classes[L.cls].second;
+        rl::KGroup g{};
+        g.n = L.cnt;
+        int blocks = 0;
+        for (int j = 0; j < L.cnt; ++j) {
+            rl_plan* p = items[L.i0 + j].p;
+            fill_kparams(p, m, p->shape_B > 0 ? p->shape_B : p->B, false, g.p[j]);
+            g.start[j] = blocks;
+            blocks += p->B;
+        }
+        for (int j = 0; j < L.cnt; ++j) HIPCHK(hipEventRecord(items[L.i0 + j].p->ev[1 + m], L.ls));
+        const hipError_t e = rl::launch_optimize_group(g, s, classes[L.cls].first[2] != 0, classes[L.cls].first[3] != 0,
+                                                       m == 1, L.ls);
+        if (e != hipSuccess) return fail(RL_EHIP, std::string("group launch: ") + hipGetErrorString(e));
+        for (int j = 0; j < L.cnt; ++j) HIPCHK(hipEventRecord(items[L.i0 + j].p->ev_end[m], L.ls));
+        ends.push_back(items[L.i0 + L.cnt - 1].p->ev_end[m]);
+    }
+    for (rl_plan* p : solo) {
+        const int rc = rl_plan_run(p, p->own_stream);
+        if (rc != RL_OK) return rc;
+        ends.push_back(p->ev[3]);
+        p->last_stream = st;
+    }
+    for (hipEvent_t e : ends) HIPCHK(hipStreamWaitEvent(st, e, 0));
+    for (int i = 0; i < n; ++i) {
+        HIPCHK(hipEventRecord(plans[i]->ev[3], st));
+        plans[i]->ran = true;
+    }
     return RL_OK;
 }
 

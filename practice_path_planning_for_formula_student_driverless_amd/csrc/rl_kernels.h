@@ -40,6 +40,16 @@ struct KParams {
     const double* hi0;
 };
 
+// Up to RL_GROUP_MAX plans of one kernel shape in one launch (rl_plan_run_group): the plans'
+// parameters and their first workgroup index, passed as kernel arguments (8 x 344 B + 36 B)
+constexpr int RL_GROUP_MAX = 8;
+struct KGroup {
+    int32_t n;                          // plans in the launch (1..RL_GROUP_MAX)
+    int32_t start[RL_GROUP_MAX];        // first workgroup of plan j; plan j has p[j].B of them
+    KParams p[RL_GROUP_MAX];
+};
+static_assert(sizeof(KGroup) <= 4096, "kernel arguments of a group launch");
+
 // The instance's completion flag: every wave waits until its own result stores have reached
 // L2 (vmcnt(0): on gfx9 a store's count drops when L2 acknowledges it), the workgroup joins,
 // then one lane writes the L2 back to memory (a system-scope release fence: buffer_wbl2 and
@@ -108,6 +118,12 @@ inline Shape lat_shape(int N) {
 Shape pick_shape(int N, int B, bool mintime, int cus);
 // enqueue one persistent launch (one workgroup per instance) on `st`
 hipError_t launch_optimize(const KParams& p, bool mintime, hipStream_t st);
+// the shapes a group launch covers (the one-wave throughput shapes, rl_kernels_group.hip)
+bool group_shape(const Shape& s);
+// one launch of g.n plans whose pick_shape is s (group_shape(s)), all closed or all open,
+// all ragged (N % K != 0) or none, one mode: rl_kernels_group.hip
+hipError_t launch_optimize_group(const KGroup& g, const Shape& s, bool closed, bool ragged, bool mintime,
+                                 hipStream_t st);
 // the launches of the latency shapes lat_shape(p.N) and of every (4, 512) shape (also the
 // min-time shape for 1024 < N <= 2048 below two instances per CU), rl_kernels_lat.hip
 hipError_t launch_optimize_lat(const KParams& p, bool mintime, hipStream_t st);

@@ -344,9 +344,10 @@ struct MinWaves {
 };
 
 // RAGGED: N % K != 0, i.e. one thread holds a partial chunk (decided per launch; the
-// exact-multiple version carries no partial-chunk bookkeeping)
+// exact-multiple version carries no partial-chunk bookkeeping).  One workgroup runs instance b
+// of the launch p; the kernels below call it with their own (p, b).
 template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
-__global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_kernel(KParams p) {
+__device__ __forceinline__ void rl_optimize_body(const KParams& p, const int b) {
     constexpr int NW = T / 64;
     constexpr bool WARM = WarmStart<T, MT>::value;
     __shared__ Smem<K, T, WARM> sm;
@@ -356,7 +357,6 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
 #endif
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int b = blockIdx.x;
     const int N = p.N;
     const int base = tid * K;
     const int Ta = (N + K - 1) / K;
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     const rl_cfg& C = p.cfg[p.ncfg == 1 ? 0 : b];
     const uint64_t seed = p.seeds ? p.seeds[b] : 0ull;
 
-    const double Lb = p.Ls ? p.Ls[blockIdx.x] : p.L;
+    const double Lb = p.Ls ? p.Ls[b] : p.L;
     // (uni: the kernel-lifetime constants live in SGPR pairs, not in VGPRs.  Besides the
     // registers this saves, it keeps them out of the register allocator's VGPR/AGPR
     // live-range copies: with this compiler such a copy can be placed inside a divergent
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
     // seen as ax = 0/(garbage 2h) = -0 on the last, partial chunk of an open track; an SGPR
     // copy is lane-independent)
     const double h = uni(Lb / (double)N);                // ref:690 / 913
-    const double* __restrict__ CEN = p.center + (size_t)blockIdx.x * (size_t)p.center_stride;
+    const double* __restrict__ CEN = p.center + (size_t)b * (size_t)p.center_stride;
     const double invh = uni(1.0 / h), inv2h = uni(1.0 / (2 * h)), invh2 = uni(1.0 / (h * h));   // ref:547, 562
     const double m2invh2 = uni(-2 * invh2);              // ref:577 (-2*invh2)
     const double two_h = uni(2 * h), hh = uni(h * h);    // ref:602-603 divisors
@@ -1679,6 +1679,27 @@ __global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_ke
         else if (wid == 1 || wid == 2) rl_dbg_stamps[b][13 + wid] = st_acc[13 + wid];
     }
 #endif
+}
+
+// one launch of one plan: workgroup b runs instance b
+template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
+__global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_kernel(KParams p) {
+    rl_optimize_body<K, T, CLOSED, MT, RAGGED>(p, blockIdx.x);
+}
+
+// one launch of up to RL_GROUP_MAX plans of one shape (rl_plan_run_group): the plans'
+// workgroups follow each other (plan j owns blocks start[j] .. start[j+1]-1), so a grid of
+// small plans fills the GPU as one launch instead of one launch per plan.  The launch
+// parameters are kernel arguments (constant memory): plan j is found and read with scalar
+// instructions, and instance b of it runs exactly as in that plan's own launch.
+template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
+__global__ __launch_bounds__(T, (MinWaves<K, T, MT>::value)) void rl_optimize_group_kernel(KGroup g) {
+    const int blk = blockIdx.x;
+    int j = 0;
+#pragma unroll
+    for (int i = 1; i < RL_GROUP_MAX; ++i)
+        if (i < g.n && blk >= g.start[i]) j = i;
+    rl_optimize_body<K, T, CLOSED, MT, RAGGED>(g.p[j], blk - g.start[j]);
 }
 
 }  // namespace rl

@@ -174,6 +174,14 @@ class Plan:
     def run(self, stream_ptr: int = 0) -> None:
         _check(_lib().rl_plan_run(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    @staticmethod
+    def run_group(plans: Sequence["Plan"], stream_ptr: int = 0) -> None:
+        """rl_plan_run_group: run the plans (one device) in as few kernel launches as their
+        shapes allow -- a sweep of small plans as a few large grids -- with results equal to
+        each plan's own run().  `stream_ptr` (0: the first plan's stream) waits for all."""
+        hs = (C.c_void_p * len(plans))(*[pl._h.value for pl in plans])
+        _check(_lib().rl_plan_run_group(hs, len(plans), C.c_void_p(stream_ptr) if stream_ptr else None))
+
     def set_shape_batch(self, shape_B: int) -> None:
         """Choose the kernel shape for a batch of shape_B instances (0 = this plan's B):
         rl_plan_set_shape_batch.  Concurrent plans on one device pass the total in flight."""

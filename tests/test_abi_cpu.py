@@ -246,6 +246,15 @@ def test_outputs_from_pool():
     assert o2.as_c().x                               # plain C pointers for the ABI
 
 
+def test_plan_run_group_checks_arguments():
+    """rl_plan_run_group refuses an empty or NULL plan list before any device call."""
+    lib = abi.load_library()
+    assert lib.rl_plan_run_group(None, 0, None) == abi.RL_EINVAL
+    arr = (C.c_void_p * 2)(None, None)
+    assert lib.rl_plan_run_group(arr, 2, None) == abi.RL_EINVAL
+    assert lib.rl_plan_run_group(arr, 0, None) == abi.RL_EINVAL
+
+
 def test_compute_fails_loudly_without_gpu():
     lib = abi.load_library()
     if lib.rl_device_count() > 0:
