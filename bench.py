@@ -438,10 +438,10 @@ def run_c3(rank, local, stream, reps: int = 3):
 def run_c4(world, rank, local, dev, dist):
     """C4: 7 bundled tracks x 512 (mu, P_max_W, lambda_smooth) points, min-curv + min-time.
     Items are sharded track-major over ranks; one plan per (track, mode), all run by one
-    rl_plan_run_group: per mode one launch per (K, N % K) class of one-wave plans, the
-    launches concurrent; laps gathered to rank 0 in item order.  (scripts/c4_group.py at the
-    box's 4 hardware queues: 13.3 ms grouped against 16.5 ms with every plan on its own
-    stream, bit-exact; profiles/r06/c4_group.log.)"""
+    rl_plan_run_group: per mode one launch per K of one-wave plans, the launches concurrent;
+    laps gathered to rank 0 in item order.  (scripts/c4_group.py at the box's 4 hardware
+    queues: 13.3 ms grouped against 16.4 ms with every plan on its own stream, bit-exact;
+    profiles/r06/c4_group.log.)"""
     import torch
 
     groups = D.c4_shard(world, rank)
@@ -465,11 +465,10 @@ def run_c4(world, rank, local, dev, dist):
                 mt_plans.append(pl)
         meta.append((t, ks, prob))
     stream = torch.cuda.Stream(device=dev)
-    launches = set()        # the group launches: one per (mode, K, N % K) class of one-wave plans
+    launches = set()        # the group launches: one per (mode, K) of one-wave plans
     for pl in plans:
         m = abi.RL_MODE_MINCURV if pl.modes & abi.RL_MODE_MINCURV else abi.RL_MODE_MINTIME
-        K, T = pl.shape(m)
-        launches.add((m, K, T, bool(K) and pl.N % K != 0))
+        launches.add((m, *pl.shape(m)))
 
     def launch():
         raceline.Plan.run_group(plans, stream.cuda_stream)
@@ -495,8 +494,8 @@ def run_c4(world, rank, local, dev, dist):
         dt, n_inst = float(allst[:, 0].max()), int(allst[:, 1].sum())
     return {"instances": int(n_inst), "modes": "min-curv + min-time", "ms": round(dt * 1e3, 3),
             "rank0_plan_shapes_KxT": shapes, "shape_batch": n_flight,
-            "schedule": f"rl_plan_run_group: {len(plans)} plans in {len(launches)} launches (one per mode, K and "
-                        f"N % K class of one-wave plans), concurrent",
+            "schedule": f"rl_plan_run_group: {len(plans)} plans in {len(launches)} launches (one per mode and K "
+                        f"of one-wave plans), concurrent",
             "tracks_per_s": round(n_inst / dt, 1), "outer_iters_per_s": round(2 * 14 * n_inst / dt, 1),
             "lap_min_s": float(laps.min()), "lap_max_s": float(laps.max())}, laps
 

@@ -221,8 +221,8 @@ int rl_plan_run(rl_plan* plan, void* hip_stream);
 /* rl_plan_run of n plans of one device in as few launches as their kernel shapes allow (a
  * sweep of many small plans: C4's 14 (track, mode) plans of 512 one-wave instances).  Every
  * (plan, mode) whose shape is a one-wave throughput shape ((4|5|8, 64): N <= 512 in a batch
- * that fills the GPU) joins one launch with the other plans of its mode, K, closed flag and
- * N % K class (up to 8 plans per launch), the instances of all of them in one grid; other
+ * that fills the GPU) joins one launch with the other plans of its mode, K and closed flag
+ * (up to 8 plans per launch), the instances of all of them in one grid; other
  * plans run as rl_plan_run.  The launches run concurrently on plan-owned streams, after
  * everything queued on `hip_stream` (NULL: the first plan's stream), which waits for all of
  * them.  Results equal each plan's own rl_plan_run bit for bit.  A plan may appear once. */

@@ -19,7 +19,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 KERNEL_SRCS = ["csrc/rl_kernels.hip", "csrc/rl_kernels_group.hip", "csrc/rl_kernels_lat.hip", "csrc/rl_kernels_mid.hip", "csrc/rl_stream.hip", "csrc/rl_geom.hip", "csrc/rl_format.hip", "csrc/rl_abi.cpp"]
-KERNEL_DEPS = KERNEL_SRCS + ["csrc/rl_optimize_body.h", "csrc/rl_kernels.h", "csrc/rl_device.h", "csrc/rl_math.h", "csrc/rl_corridor.h"]
+KERNEL_DEPS = KERNEL_SRCS + ["csrc/rl_optimize_body.h", "csrc/rl_optimize_body.inc", "csrc/rl_kernels.h", "csrc/rl_device.h", "csrc/rl_math.h", "csrc/rl_corridor.h"]
 # -ffp-contract=off: HIP defaults to fusing a*b+c into FMA, which would change
 # the reference's roundings.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
@@ -32,8 +32,8 @@ HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contr
 # iterative occupancy scheduler; the streaming kernel keeps the default
 TU_FLAGS = {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"],
             "csrc/rl_kernels_group.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"],
-            "csrc/rl_kernels_lat.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-            "csrc/rl_kernels_mid.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+            "csrc/rl_kernels_lat.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-DRL_BODY_CALL=0"],
+            "csrc/rl_kernels_mid.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp", "-DRL_BODY_CALL=0"]}
 
 
 def _stale(target: str, deps) -> bool:

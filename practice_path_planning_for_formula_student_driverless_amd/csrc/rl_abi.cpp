@@ -665,7 +665,7 @@ int rl_plan_run(rl_plan* p, void* hip_stream) {
 
 // rl_plan_run of n plans (one device) as few launches as their shapes allow: every (plan,
 // mode) whose kernel shape is a one-wave throughput shape (rl::group_shape) joins the group
-// launch of its (mode, K, closed, ragged) class, up to RL_GROUP_MAX plans per launch; the
+// launch of its (mode, K, closed) class, up to RL_GROUP_MAX plans per launch; the
 // other plans run as rl_plan_run on their own streams.  The launches run concurrently, each
 // on a plan-owned stream after everything queued on `hip_stream`, which waits for all of
 // them.  Results equal each plan's own rl_plan_run bit for bit (the same instance code, the
@@ -686,19 +686,22 @@ int rl_plan_run_group(rl_plan* const* plans, int32_t n, void* hip_stream) {
         rl_plan* p;
         int m;
     };
-    // class key: mode, K, closed, ragged
-    std::vector<std::pair<std::array<int, 4>, std::vector<Item>>> classes;
+    // class key: mode, K, closed.  A launch whose plans include a ragged N (N % K != 0) runs
+    // the ragged form for all of them (it covers every N, bit for bit): one launch per class
+    // instead of two (C4: 4 launches, all concurrent at 4 HW queues; 13.25 against 13.52 ms
+    // split by N % K, profiles/r06/c4_group.log)
+    std::vector<std::pair<std::array<int, 3>, std::vector<Item>>> classes;
     std::vector<rl_plan*> solo;
     for (int i = 0; i < n; ++i) {
         rl_plan* p = plans[i];
         const int sB = p->shape_B > 0 ? p->shape_B : p->B;
         bool ok = !p->stream && p->N > 0 && p->max_outer > 0 && (p->modes & 3);
-        std::array<int, 4> key[2];
+        std::array<int, 3> key[2];
         for (int m = 0; m < 2 && ok; ++m) {
             if (!(p->modes & (1 << m))) continue;
             const rl::Shape s = rl::pick_shape(p->N, sB, m == 1, cus);
             ok = rl::group_shape(s);
-            key[m] = {m, s.K, p->closed ? 1 : 0, p->N % s.K ? 1 : 0};
+            key[m] = {m, s.K, p->closed ? 1 : 0};
         }
         if (!ok) {
             solo.push_back(p);
@@ -749,15 +752,16 @@ int rl_plan_run_group(rl_plan* const* plans, int32_t n, void* hip_stream) {
         rl::KGroup g{};
         g.n = L.cnt;
         int blocks = 0;
+        bool ragged = false;
         for (int j = 0; j < L.cnt; ++j) {
             rl_plan* p = items[L.i0 + j].p;
             fill_kparams(p, m, p->shape_B > 0 ? p->shape_B : p->B, false, g.p[j]);
             g.start[j] = blocks;
             blocks += p->B;
+            ragged |= p->N % s.K != 0;
         }
         for (int j = 0; j < L.cnt; ++j) HIPCHK(hipEventRecord(items[L.i0 + j].p->ev[1 + m], L.ls));
-        const hipError_t e = rl::launch_optimize_group(g, s, classes[L.cls].first[2] != 0, classes[L.cls].first[3] != 0,
-                                                       m == 1, L.ls);
+        const hipError_t e = rl::launch_optimize_group(g, s, classes[L.cls].first[2] != 0, ragged, m == 1, L.ls);
         if (e != hipSuccess) return fail(RL_EHIP, std::string("group launch: ") + hipGetErrorString(e));
         for (int j = 0; j < L.cnt; ++j) HIPCHK(hipEventRecord(items[L.i0 + j].p->ev_end[m], L.ls));
         ends.push_back(items[L.i0 + L.cnt - 1].p->ev_end[m]);

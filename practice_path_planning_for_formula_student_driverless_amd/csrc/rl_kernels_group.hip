@@ -40,7 +40,8 @@ hipError_t launch_optimize_group(const KGroup& g, const Shape& s, bool closed, b
     for (int j = 0; j < g.n; ++j) {
         const KParams& p = g.p[j];
         // every plan of the launch in the shape, boundary and chunk form it was compiled for
-        if (p.N <= 0 || p.N > s.K * s.T || p.B < 1 || (p.closed != 0) != closed || (p.N % s.K != 0) != ragged)
+        // (the ragged form covers every N; the exact-multiple form only N % K == 0)
+        if (p.N <= 0 || p.N > s.K * s.T || p.B < 1 || (p.closed != 0) != closed || (!ragged && p.N % s.K != 0))
             return hipErrorInvalidValue;
     }
     if (s.K == 4) return launch_gk<4>(g, closed, ragged, mintime, st);

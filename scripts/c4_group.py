@@ -2,7 +2,9 @@
 """C4 as the bench runs it (7 bundled tracks x 512 sweep points x 2 modes = 14 single-mode
 plans, shape batch 7168) under two schedules, interleaved rounds, wall ms of the whole sweep:
   s14    every plan on its own HIP stream (bench.run_c4 before rl_plan_run_group)
-  group  rl_plan_run_group over the 14 plans: per mode one launch per (K, N % K) class
+  group  rl_plan_run_group over the 14 plans: per mode one launch per K (the ragged form
+         for a launch with any N % K != 0; profiles/r06/c4_group.log also holds the earlier
+         split by N % K as `group` against this merged form as `group_mix`)
 and a bit-for-bit check of every plan's laps and counters between the two.
 usage: python scripts/c4_group.py [rounds]   (GPU_MAX_HW_QUEUES as the environment sets it)"""
 import os
@@ -56,16 +58,18 @@ def snapshot():
 
 s14()
 ref = snapshot()
-group()
-got = snapshot()
-same = all(all(np.array_equal(a, b) for a, b in zip(r, g)) for r, g in zip(ref, got))
+same = {}
+for name, f in (("group", group),):
+    f()
+    got = snapshot()
+    same[name] = all(all(np.array_equal(a, b) for a, b in zip(r, g)) for r, g in zip(ref, got))
 res = {"s14": [], "group": []}
 for _ in range(rounds):
     for name, f in (("s14", s14), ("group", group)):
         t0 = time.perf_counter()
         f()
         res[name].append((time.perf_counter() - t0) * 1e3)
-print(f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')}; bit-exact group vs s14: {same}")
+print(f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')}; bit-exact vs s14: {same}")
 for k, v in res.items():
     print(f"C4 {k:6s} wall ms: median {np.median(v):7.2f} min {np.min(v):7.2f}", flush=True)
 for pl in plans:
