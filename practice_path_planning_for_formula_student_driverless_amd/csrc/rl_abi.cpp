@@ -717,6 +717,10 @@ int rl_plan_run_group(rl_plan* const* plans, int32_t n, void* hip_stream) {
             it->second.push_back({p, m});
         }
     }
+    // the plans of a class longest first (by N): the grid dispatches its workgroups in order,
+    // so its last ones are the shorter instances (C4 13.39 -> 13.14 ms, profiles/r06/c4_group.log)
+    for (auto& c : classes)
+        std::stable_sort(c.second.begin(), c.second.end(), [](const Item& x, const Item& y) { return x.p->N > y.p->N; });
     // the launches: class chunks of up to RL_GROUP_MAX plans, then the solo plans
     struct Launch {
         int cls;

@@ -4,7 +4,8 @@ plans, shape batch 7168) under two schedules, interleaved rounds, wall ms of the
   s14    every plan on its own HIP stream (bench.run_c4 before rl_plan_run_group)
   group  rl_plan_run_group over the 14 plans: per mode one launch per K (the ragged form
          for a launch with any N % K != 0; profiles/r06/c4_group.log also holds the earlier
-         split by N % K as `group` against this merged form as `group_mix`)
+         split by N % K as `group` against this merged form as `group_mix`, and the merged
+         form in plan order as `group` against longest-first as `group_sorted`, now the default)
 and a bit-for-bit check of every plan's laps and counters between the two.
 usage: python scripts/c4_group.py [rounds]   (GPU_MAX_HW_QUEUES as the environment sets it)"""
 import os
