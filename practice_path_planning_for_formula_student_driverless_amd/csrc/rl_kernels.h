@@ -66,6 +66,20 @@ __device__ __forceinline__ void signal_done(uint32_t* done, int b, uint32_t epoc
     }
 }
 
+// Wave priority by progress, set at the top of every outer iteration (`mode` 1: four levels,
+// 3 in the first quarter of the instance's outer iterations down to 0 in the last; 2: two
+// levels, 3 in the first half, 0 after).  Two instances share a CU (two per CU in C2's shape);
+// the arbiter issues the oldest wave first at equal priority, so the first-dispatched
+// instance of each pair races ahead and the last instance of every CU runs alone at the
+// grid's end.  Favouring the instance that is behind makes the pair end together.
+__device__ __forceinline__ void progress_prio(int outer, int MO, int mode) {
+    const int lvl = mode == 2 ? (2 * outer < MO ? 3 : 0) : ((MO - outer) * 4) / (MO + 1);
+    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 // Per-instance HBM state of the large-N streaming kernel (rl_stream.hip): RL_STREAM_ARRAYS
 // arrays of N doubles per instance, instance-major [B][RL_STREAM_ARRAYS][N] in one allocation
 // (al, an, gr, lo, hi, a1, a2, n0, w, q1, q2, d1, g2, v, vs), so one buffer resource and a

@@ -346,6 +346,11 @@ struct MinWaves {
 // RAGGED: N % K != 0, i.e. one thread holds a partial chunk (decided per launch; the
 // exact-multiple version carries no partial-chunk bookkeeping).  One workgroup runs instance b
 // of the launch p; the kernels below call it with their own (p, b).
+#ifndef RL_PRIO
+// wave priority by progress (rl_kernels.h progress_prio): build.py sets 1 for the throughput
+// shapes' translation units (two or more instances per CU); 0 keeps the issue order
+#define RL_PRIO 0
+#endif
 template <int K, int T, bool CLOSED, bool MT, bool RAGGED>
 __device__ __forceinline__ void rl_optimize_body(const KParams& p, const int b) {
 #define RL_BID_ b

@@ -28,6 +28,10 @@
 #include "rl_kernels.h"
 #include "rl_math.h"
 
+#ifndef RL_SPRIO
+#define RL_SPRIO 0         // (A/B build knob: wave priority by progress, rl_kernels.h progress_prio)
+#endif
+
 namespace rl {
 
 namespace {
@@ -706,6 +710,9 @@ __global__ __launch_bounds__(TS) void rl_stream_kernel(KParams p, StreamBufs sb)
     auto an_p = AN;
     RL_SSTAMP(0);
     for (int outer = 0;; ++outer) {
+#if RL_SPRIO
+        progress_prio(outer, MO, RL_SPRIO);                        // (tail balance, rl_kernels.h)
+#endif
         __syncthreads();
         if (outer > 0) {                                           // ref:743-746
             for (int i = opq(tid); i < N; i += TS) {

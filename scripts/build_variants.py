@@ -65,6 +65,9 @@ VARIANTS = {
     "stream_iilp": {"_tu": {"csrc/rl_stream.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}},
     "btfmt": {"RL_BT_FIRST_MT": 1, "RL_BT_ADAPT": 0},
     "btfixed": {"RL_BT_ADAPT": 0},
+    "prio": {"RL_PRIO": 1},              # wave priority falling with the outer iteration (tail balance)
+    "prio2": {"RL_PRIO": 2},             # the same with two levels
+    "prio_s": {"RL_PRIO": 1, "RL_SPRIO": 1},   # and in the streaming kernel
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "stamps_eval": {"RL_STAMPS": 1, "RL_STAMPS_EVAL": 1},   # + the latency evaluation's phases (scripts/stamps_lat.py)
     "count": {"RL_COUNT": 1},            # diagnostic (scripts/counts_c5.py); not A/B-timed
