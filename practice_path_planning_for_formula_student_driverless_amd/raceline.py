@@ -179,6 +179,8 @@ class Plan:
         """rl_plan_run_group: run the plans (one device) in as few kernel launches as their
         shapes allow -- a sweep of small plans as a few large grids -- with results equal to
         each plan's own run().  `stream_ptr` (0: the first plan's stream) waits for all."""
+        if not plans or any(getattr(pl, "_h", None) is None for pl in plans):
+            raise ValueError("run_group: no plans, or a closed plan")
         hs = (C.c_void_p * len(plans))(*[pl._h.value for pl in plans])
         _check(_lib().rl_plan_run_group(hs, len(plans), C.c_void_p(stream_ptr) if stream_ptr else None))
 

@@ -255,6 +255,16 @@ def test_plan_run_group_checks_arguments():
     assert lib.rl_plan_run_group(arr, 0, None) == abi.RL_EINVAL
 
 
+def test_run_group_refuses_closed_plans():
+    """raceline.Plan.run_group checks its plan list before any library call."""
+    class Closed:
+        _h = None
+    with pytest.raises(ValueError):
+        raceline.Plan.run_group([])
+    with pytest.raises(ValueError):
+        raceline.Plan.run_group([Closed()])
+
+
 def test_compute_fails_loudly_without_gpu():
     lib = abi.load_library()
     if lib.rl_device_count() > 0:
