@@ -30,11 +30,12 @@ HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contr
 # B=1 training_map min-curv 1.43 -> 1.31 ms, C3-shaped min-time 4.73 -> 4.31
 # ms); the throughput kernels were slower under max-ilp and gain ~0.2-2 % from the
 # iterative occupancy scheduler; the streaming kernel keeps the default
-# RL_PRIO=1 (rl_kernels.h progress_prio): the throughput shapes, two or more instances per
-# CU, raise the priority of the instance that is behind (C2 8.35 -> 8.03 ms, C4's one-wave
-# shape -8 %, profiles/r06/ab_prio.log); the latency shapes hold one instance per CU
-TU_FLAGS = {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", "-DRL_PRIO=1"],
-            "csrc/rl_kernels_group.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", "-DRL_PRIO=1"],
+# RL_PRIO=3 (rl_kernels.h progress_prio): the throughput shapes, two or more instances per
+# CU, raise the priority of the instance that is behind (C2 8.35 -> 8.03 -> 7.96 ms, C4's
+# one-wave shape -8..-10 %, profiles/r06/ab_prio.log, ab_prio3.log); the latency shapes hold
+# one instance per CU
+TU_FLAGS = {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", "-DRL_PRIO=3"],
+            "csrc/rl_kernels_group.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", "-DRL_PRIO=3"],
             "csrc/rl_kernels_lat.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-DRL_BODY_CALL=0"],
             "csrc/rl_kernels_mid.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp", "-DRL_BODY_CALL=0"]}
 

@@ -73,7 +73,13 @@ __device__ __forceinline__ void signal_done(uint32_t* done, int b, uint32_t epoc
 // instance of each pair races ahead and the last instance of every CU runs alone at the
 // grid's end.  Favouring the instance that is behind makes the pair end together.
 __device__ __forceinline__ void progress_prio(int outer, int MO, int mode) {
-    const int lvl = mode == 2 ? (2 * outer < MO ? 3 : 0) : ((MO - outer) * 4) / (MO + 1);
+    // mode 3 (the product's, build.py): the levels' resolution spent near the end, where the
+    // pair's gap decides the tail: 3 for the first half, 2 to three quarters, 1 to the last
+    // outer iteration, 0 in it (C2 -0.7..-1 % against mode 1; mode 2 and an even later
+    // split were slower: profiles/r06/ab_prio.log, ab_prio3.log)
+    const int lvl = mode == 2   ? (2 * outer < MO ? 3 : 0)
+                    : mode == 3 ? (2 * outer < MO ? 3 : 4 * outer < 3 * MO ? 2 : outer < MO - 1 ? 1 : 0)
+                                : ((MO - outer) * 4) / (MO + 1);
     if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
     else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
     else if (lvl == 1) __builtin_amdgcn_s_setprio(1);

@@ -67,6 +67,8 @@ VARIANTS = {
     "btfixed": {"RL_BT_ADAPT": 0},
     "prio": {"RL_PRIO": 1},              # wave priority falling with the outer iteration (tail balance)
     "prio2": {"RL_PRIO": 2},             # the same with two levels
+    "prio3": {"RL_PRIO": 3, "_tu": {"csrc/rl_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"],
+                                    "csrc/rl_kernels_group.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]}},   # end-weighted levels
     "prio_s": {"RL_PRIO": 1, "RL_SPRIO": 1},   # and in the streaming kernel
     "stamps": {"RL_STAMPS": 1},          # diagnostic (scripts/stamps.py); not A/B-timed
     "stamps_eval": {"RL_STAMPS": 1, "RL_STAMPS_EVAL": 1},   # + the latency evaluation's phases (scripts/stamps_lat.py)
