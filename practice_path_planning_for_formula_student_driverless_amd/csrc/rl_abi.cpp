@@ -1511,7 +1511,11 @@ int download_overlapped(CacheEntry* e, rl_plan* p, const std::vector<CopyJob> (&
             if (joined[g.m]) break;
             const hipError_t q = hipEventQuery(p->ev_end[g.m]);
             if (q == hipSuccess) {
-                // the kernel has ended without this flag: stream order from here on
+                // the kernel has ended: every flag it stored is visible now, so a flag that
+                // arrived between the read above and the query counts as signalled
+                while (b < g.b1 && fl[(size_t)g.m * B + b] == epoch) ++b;
+                if (b == g.b1) break;
+                // ended without this flag: stream order from here on
                 if (hipStreamWaitEvent(e->dl, p->ev_end[g.m], 0) != hipSuccess) bad = true;
                 joined[g.m] = true;
                 break;
