@@ -66,7 +66,7 @@ if "--commit" in sys.argv and "hbm_bytes_per_launch" in der:
     from bench import source_sha
 
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    os.makedirs(os.path.dirname(p), exist_ok=True)     # profiles/ does not travel to the GPU box
+    os.makedirs(os.path.dirname(p), exist_ok=True)     # (on the GPU box profiles/r0*/ are not uploaded: .gpurunignore)
     d = json.load(open(p)) if os.path.exists(p) else {}
     key = sys.argv[sys.argv.index("--key") + 1] if "--key" in sys.argv else "c2_mincurv"
     prof = sys.argv[sys.argv.index("--profile") + 1] if "--profile" in sys.argv else out
